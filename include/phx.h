@@ -1,0 +1,182 @@
+/*
+ * phx.h — C ABI of the MI355X-native scenario-batched PH engine (libphx.so).
+ *
+ * The reference (garg02/mpi-sppy) is pure Python; its PH hot path reaches
+ * native code only through an external LP/QP solver behind Pyomo
+ * (SPOpt.solve_one, mpisppy/spopt.py:85-223, solver call at :165-172) and
+ * through mpi4py collectives.  This header is the drop-in boundary that
+ * replaces those per-scenario calls and Python loops with batched HIP kernels
+ * over all local scenarios at once.  Each entry point cites the reference
+ * interface it replaces.
+ *
+ * Conventions
+ *   - Every array argument is a DEVICE pointer (hipMalloc / torch.cuda memory)
+ *     unless the name ends in _host.  Per-scenario arrays are scenario-minor:
+ *     element i of local scenario s lives at [i*S + s].
+ *   - fp64 everywhere; infinite bounds are IEEE +-inf.
+ *   - Every function returns 0 on success, nonzero on failure; the message is
+ *     available from phx_last_error(ctx).  No C++ exception crosses the ABI.
+ *   - Ownership: the caller owns every array it passes; the context owns only
+ *     its own scratch (solver state, scaled copies, polish workspace).
+ *   - Threading: one host thread per context.  Work is ordered on the HIP
+ *     stream passed in (hipStream_t as void*; NULL = default stream).  Only
+ *     phx_set_problem and phx_solve synchronise with the host (documented).
+ */
+#ifndef PHX_H
+#define PHX_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct phx_ctx phx_ctx;
+
+/* Per-scenario LP/QP standard form with a pattern shared by all scenarios:
+ *      min  c'x + qN'x_N + 0.5 pN' x_N^2     (qN, pN: PH terms, phx_set_ph_terms)
+ *      s.t. bl <= A x <= bu,  lb <= x <= ub
+ * Replaces what the reference extracts from each Pyomo scenario model
+ * (SPBase._create_scenarios, spbase.py:255-291) and the PH objective terms of
+ * PHBase.attach_PH_to_objective (phbase.py:617-699).                         */
+typedef struct phx_problem_desc {
+    int32_t S;              /* local scenarios (lanes)                         */
+    int32_t n, m, nnz;      /* columns, rows, nonzeros per scenario            */
+    int32_t N;              /* nonant slots per scenario                       */
+    int32_t nvar;           /* number of scenario-varying A entries            */
+    const int32_t* rowptr;  /* [m+1]  CSR pattern                              */
+    const int32_t* colidx;  /* [nnz]                                           */
+    const int32_t* kvar;    /* [nnz]  -1: value Aconst[k] for all scenarios;
+                                      v>=0: value Avar[v*S+s]                  */
+    const double* Aconst;   /* [nnz]                                           */
+    const double* Avar;     /* [nvar*S]                                        */
+    const double* c;        /* [n] or [n*S] (c_vary)                           */
+    const double* lb;       /* [n] or [n*S] (bnd_vary)                         */
+    const double* ub;
+    const double* bl;       /* [m] or [m*S] (rhs_vary)                         */
+    const double* bu;
+    int32_t c_vary, bnd_vary, rhs_vary;
+    const int32_t* slot_col;/* [N]  column of each nonant slot, in the
+                               reference's nonant order (spbase.py:293-302)   */
+} phx_problem_desc;
+
+/* Solver knobs; the engine fills them from options["iter0_solver_options"] /
+ * ["iterk_solver_options"] (phbase.py:273-275).                              */
+typedef struct phx_solve_opts {
+    int32_t max_iters;        /* PDHG iterations before giving up (per solve) */
+    int32_t check_every;      /* PDHG iterations per launch between checks    */
+    int32_t restart_max;      /* artificial Halpern restart length            */
+    int32_t polish;           /* 1: active-set KKT polish (exact optimum)     */
+    int32_t refine_steps;     /* iterative-refinement steps in the polish     */
+    int32_t warm_start;       /* 1: start from the previous solution          */
+    double  polish_below;     /* attempt a polish once rel. KKT err < this    */
+    double  opt_tol;          /* accept unpolished point when rel. KKT < this */
+    double  kkt_tol;          /* polish certificate tolerance (relative)      */
+    double  reg;              /* polish regularisation (scaled units)         */
+} phx_solve_opts;
+
+/* Scenario-tree reduction layout for Compute_Xbar (phbase.py:27-107): for each
+ * tile, the nonant slots [slot_lo, slot_lo+nlen) of one tree node summed over
+ * the contiguous local scenarios [s_begin, s_end).  Tiles of one node are
+ * consecutive; node_tile_ptr[v]..node_tile_ptr[v+1] lists them.             */
+typedef struct phx_tree_desc {
+    int32_t ntiles;
+    const int32_t* tile_s0;    /* [ntiles] */
+    const int32_t* tile_s1;    /* [ntiles] */
+    const int32_t* tile_slot;  /* [ntiles] first slot                        */
+    const int32_t* tile_nlen;  /* [ntiles] slots of the node                  */
+    const int32_t* tile_out;   /* [ntiles] offset into the partial buffer     */
+    int32_t nnodes;            /* nodes with at least one local scenario      */
+    const int32_t* node_tile_ptr; /* [nnodes+1]                               */
+    const int32_t* node_off;   /* [nnodes] offset of the node's slots in the
+                                  global node-slot vector (length NNS)        */
+    const int32_t* node_nlen;  /* [nnodes]                                    */
+    int32_t NNS;               /* global number of (node, slot) entries       */
+    int32_t npart;             /* size of the partial buffer (doubles)        */
+} phx_tree_desc;
+
+/* ---- lifetime ---------------------------------------------------------- */
+int         phx_create(int32_t device, phx_ctx** out);
+int         phx_destroy(phx_ctx* ctx);
+const char* phx_last_error(const phx_ctx* ctx);
+/* Number of compiled gfx targets / a build string, for diagnostics.        */
+const char* phx_build_info(void);
+
+/* Replaces the per-scenario model build + SolverFactory/set_instance
+ * (SPOpt._create_solvers, spopt.py:839-903).  Copies/derives: CSC view,
+ * Ruiz + Pock-Chambolle scaling, per-scenario ||A||_2 (power iteration),
+ * polish workspace.  Synchronises the device (setup only).                 */
+int phx_set_problem(phx_ctx* ctx, const phx_problem_desc* desc);
+
+/* PH objective terms for the next solve (attach_PH_to_objective,
+ * phbase.py:617-699; W_on/prox_on toggles :409-440):
+ *   qN[j][s] = W_on*W[j][s] - prox_on*rho[j][s]*xbar(s,j)
+ *   pN[j][s] = prox_on*rho[j][s]
+ *   kN[s]    = prox_on*sum_j rho/2*xbar^2
+ * with xbar(s,j) = xbar_node[xbar_idx[j*S+s]].  W/rho/xbar may be NULL when
+ * W_on = prox_on = 0 (Iter0).                                              */
+int phx_set_ph_terms(phx_ctx* ctx, const double* W, const double* rho,
+                     const double* xbar_node, const int32_t* xbar_idx,
+                     int32_t W_on, int32_t prox_on, void* stream);
+
+/* Batched subproblem solve — replaces PHBase.solve_loop -> SPOpt.solve_loop ->
+ * solve_one (phbase.py:494-568, spopt.py:226-307, :85-223).  Restarted
+ * reflected-Halpern PDHG on the scaled problem, warm-started, followed by an
+ * active-set KKT polish that certifies each scenario's optimum.
+ * Outputs (all [.][S]): x_out[n], y_out[m] (row duals), obj_out[S] (objective
+ * incl. PH terms, = outer bound), status_out[S] (1 optimal, 2 iteration limit,
+ * 3 numerical failure), iters_out[S].  *total_iters_host = iterations run.
+ * Synchronises with the host once per check_every iterations.              */
+int phx_solve(phx_ctx* ctx, const phx_solve_opts* opts,
+              double* x_out, double* y_out, double* obj_out,
+              int32_t* status_out, int32_t* iters_out,
+              int32_t* total_iters_host, void* stream);
+
+/* Objective of the caller's point x ([n][S], unscaled) under the PH terms last
+ * set by phx_set_ph_terms: obj[s] = c'x + qN'x_N + 0.5 pN x_N^2 + kN — what
+ * the reference evaluates as pyo.value(objective) in Eobjective
+ * (spopt.py:327-343).                                                      */
+int phx_objective(phx_ctx* ctx, const double* x, double* obj_out, void* stream);
+
+/* Compute_Xbar local part (phbase.py:54-80): node_sums[e] = sum over local
+ * scenarios of prob_coeff*x, node_sums[NNS+e] = sum prob_coeff*x^2 for every
+ * (node, slot) entry e (zeros for nodes absent locally).  The caller then
+ * all-reduces node_sums over ranks (phbase.py:83-87) — one RCCL call.      */
+int phx_xbar(phx_ctx* ctx, const phx_tree_desc* tree, const double* x,
+             const double* prob_coeff, double* partial, double* node_sums,
+             void* stream);
+
+/* Update_W + convergence_diff local part (phbase.py:293-343):
+ *   W[j][s] += rho[j][s]*(x_N - xbar)   (if update_w)
+ *   dsum[s]  = sum_j |x_N - xbar|
+ * then seg_sums[r] = sum of dsum over local scenarios [seg_s0[r], seg_s1[r])
+ * (one segment per emulated reference rank, sputils.py:803-810).           */
+int phx_update_w(phx_ctx* ctx, const double* x, const double* xbar_node,
+                 const int32_t* xbar_idx, const double* rho, double* W,
+                 int32_t update_w, double* dsum, int32_t nseg,
+                 const int32_t* seg_s0_host, const int32_t* seg_s1_host,
+                 double* seg_sums, void* stream);
+
+/* Expectations (Eobjective/Ebound/_update_E1/feas_prob, spopt.py:310-439):
+ * out[0] = sum_s p_s*obj_s, out[1] = sum_s p_s, out[2] = sum_s p_s*[status==1]
+ * over local scenarios (deterministic tree order).  out is a device [3].    */
+int phx_expect(phx_ctx* ctx, const double* prob, const double* obj,
+               const int32_t* status, double* out, void* stream);
+
+/* Scenario-major export of a [N][S] slot array (W or nonant x) into
+ * out[S*N + 0..] — the flat layout of PHBase._populate_W_cache /
+ * PHHub.send_nonants (phbase.py:346-366, hub.py:562-577).                  */
+int phx_export_slots(phx_ctx* ctx, const double* src, double* out, void* stream);
+
+/* Timing of the most recent phx_solve: summed kernel milliseconds of the PDHG
+ * chunk launches (HIP events on the solve stream), their count, the
+ * scenario-iterations they performed (sum over launches of running lanes x
+ * check_every) and the polish milliseconds.                                */
+int phx_last_solve_timing(const phx_ctx* ctx, double* pdhg_ms_host,
+                          int32_t* pdhg_launches_host, double* lane_iters_host,
+                          double* polish_ms_host);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PHX_H */

@@ -1,0 +1,121 @@
+"""ctypes binding of the phx C ABI (include/phx.h).
+
+The product path loads ``libphx.so`` (built in-tree by ``build.py`` for
+gfx950) and raises immediately if it is missing or no GPU is visible — there
+is no CPU fallback.  The same wrapper can bind a library exporting the ABI
+under another symbol prefix; the CPU test-suite uses that to bind the
+test-only host emulation in ``tests/emu`` (never used by the product).
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libphx.so")
+
+c_int32 = ctypes.c_int32
+c_double = ctypes.c_double
+c_void_p = ctypes.c_void_p
+P_i32 = ctypes.POINTER(ctypes.c_int32)
+P_f64 = ctypes.POINTER(ctypes.c_double)
+
+
+class ProblemDesc(ctypes.Structure):
+    _fields_ = [
+        ("S", c_int32), ("n", c_int32), ("m", c_int32), ("nnz", c_int32),
+        ("N", c_int32), ("nvar", c_int32),
+        ("rowptr", c_void_p), ("colidx", c_void_p), ("kvar", c_void_p),
+        ("Aconst", c_void_p), ("Avar", c_void_p),
+        ("c", c_void_p), ("lb", c_void_p), ("ub", c_void_p),
+        ("bl", c_void_p), ("bu", c_void_p),
+        ("c_vary", c_int32), ("bnd_vary", c_int32), ("rhs_vary", c_int32),
+        ("slot_col", c_void_p),
+    ]
+
+
+class SolveOpts(ctypes.Structure):
+    _fields_ = [
+        ("max_iters", c_int32), ("check_every", c_int32), ("restart_max", c_int32),
+        ("polish", c_int32), ("refine_steps", c_int32), ("warm_start", c_int32),
+        ("polish_below", c_double), ("opt_tol", c_double), ("kkt_tol", c_double),
+        ("reg", c_double),
+    ]
+
+
+class TreeDesc(ctypes.Structure):
+    _fields_ = [
+        ("ntiles", c_int32),
+        ("tile_s0", c_void_p), ("tile_s1", c_void_p), ("tile_slot", c_void_p),
+        ("tile_nlen", c_void_p), ("tile_out", c_void_p),
+        ("nnodes", c_int32),
+        ("node_tile_ptr", c_void_p), ("node_off", c_void_p), ("node_nlen", c_void_p),
+        ("NNS", c_int32), ("npart", c_int32),
+    ]
+
+
+# every symbol of include/phx.h (tests check the library exports all of them)
+SYMBOLS = [
+    "create", "destroy", "last_error", "build_info", "set_problem", "set_ph_terms",
+    "solve", "objective", "xbar", "update_w", "expect", "export_slots", "last_solve_timing",
+]
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+class Lib:
+    """Typed handle on a library exporting the phx ABI under ``prefix``."""
+
+    def __init__(self, path=LIB_PATH, prefix="phx_"):
+        if not os.path.exists(path):
+            raise NativeError(
+                "libphx not found at %s — build it first (python -c 'import __graft_entry__ as g; "
+                "g.build()'); the engine has no CPU fallback" % path)
+        self.path = path
+        self.prefix = prefix
+        self.lib = ctypes.CDLL(path)
+        L = self.lib
+
+        def fn(name, res, args):
+            f = getattr(L, prefix + name)
+            f.restype = res
+            f.argtypes = args
+            return f
+
+        self.create = fn("create", ctypes.c_int, [c_int32, ctypes.POINTER(c_void_p)])
+        self.destroy = fn("destroy", ctypes.c_int, [c_void_p])
+        self.last_error = fn("last_error", ctypes.c_char_p, [c_void_p])
+        self.build_info = fn("build_info", ctypes.c_char_p, [])
+        self.set_problem = fn("set_problem", ctypes.c_int, [c_void_p, ctypes.POINTER(ProblemDesc)])
+        self.set_ph_terms = fn("set_ph_terms", ctypes.c_int,
+                               [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p])
+        self.solve = fn("solve", ctypes.c_int,
+                        [c_void_p, ctypes.POINTER(SolveOpts), c_void_p, c_void_p, c_void_p, c_void_p,
+                         c_void_p, P_i32, c_void_p])
+        self.objective = fn("objective", ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p])
+        self.xbar = fn("xbar", ctypes.c_int,
+                       [c_void_p, ctypes.POINTER(TreeDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p])
+        self.update_w = fn("update_w", ctypes.c_int,
+                           [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,
+                            c_int32, P_i32, P_i32, c_void_p, c_void_p])
+        self.expect = fn("expect", ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p])
+        self.export_slots = fn("export_slots", ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p])
+        self.last_solve_timing = fn("last_solve_timing", ctypes.c_int,
+                                    [c_void_p, P_f64, P_i32, P_f64, P_f64])
+
+    def check(self, ctx, rc, what):
+        if rc != 0:
+            msg = self.last_error(ctx) if ctx else None
+            raise NativeError("%s%s failed (rc=%d): %s" % (self.prefix, what, rc,
+                                                          msg.decode() if msg else "?"))
+
+
+_LIB = None
+
+
+def load():
+    """The product library (cached).  Raises NativeError if unavailable."""
+    global _LIB
+    if _LIB is None:
+        _LIB = Lib(LIB_PATH, "phx_")
+    return _LIB

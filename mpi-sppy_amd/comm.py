@@ -1,0 +1,91 @@
+"""Communicator: the engine's replacement for ``mpisppy.MPI`` (MPI.py:3-82).
+
+One process per GPU; collectives go through ``torch.distributed`` — backend
+"nccl" (= RCCL over xGMI on ROCm) when tensors live on the GPU, "gloo" for the
+CPU multi-process tests.  Without an initialised process group the
+communicator is a single-rank stand-in (the reference's ``_MockMPIComm``,
+MPI.py:19-82: rank 0, size 1, Allreduce copies).
+
+Only what the PH path needs: an in-place SUM allreduce of one fused fp64
+buffer per PH step (replacing the per-tree-node ``comms[ndn].Allreduce`` of
+phbase.py:83-87 and the scalar reductions of phbase.py:341 and
+spopt.py:341-466), barrier, and host-object gather/broadcast for setup checks.
+"""
+import os
+
+import torch
+import torch.distributed as dist
+
+
+class Comm:
+    def __init__(self, group=None):
+        self.group = group
+        if dist.is_available() and dist.is_initialized():
+            self.rank = dist.get_rank(group)
+            self.size = dist.get_world_size(group)
+            self.backend = dist.get_backend(group)
+        else:
+            self.rank = 0
+            self.size = 1
+            self.backend = None
+
+    # mpi4py-style accessors used by the reference API
+    def Get_rank(self):
+        return self.rank
+
+    def Get_size(self):
+        return self.size
+
+    def allreduce_(self, t):
+        """In-place SUM over ranks of a torch tensor (no-op on one rank)."""
+        if self.size > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        return t
+
+    def allreduce_max_(self, t):
+        if self.size > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return t
+
+    def Barrier(self):
+        if self.size > 1:
+            dist.barrier(group=self.group)
+
+    barrier = Barrier
+
+    def allgather_object(self, obj):
+        if self.size == 1:
+            return [obj]
+        out = [None] * self.size
+        dist.all_gather_object(out, obj, group=self.group)
+        return out
+
+    def gather(self, obj, root=0):
+        allv = self.allgather_object(obj)
+        return allv if self.rank == root else None
+
+    def bcast(self, obj, root=0):
+        if self.size == 1:
+            return obj
+        lst = [obj]
+        dist.broadcast_object_list(lst, src=root, group=self.group)
+        return lst[0]
+
+
+def world():
+    return Comm()
+
+
+def init_from_env(device_type="cuda"):
+    """Initialise torch.distributed from torchrun's env vars (RANK/WORLD_SIZE/...).
+    Backend "nccl" (RCCL) for GPU tensors, "gloo" for CPU.  Returns Comm."""
+    if dist.is_initialized():
+        return Comm()
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    if ws > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        backend = "nccl" if device_type == "cuda" else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        dist.init_process_group(backend=backend)
+    return Comm()

@@ -1,0 +1,387 @@
+"""PHBase — the PH iterate on the GPU behind the reference API.
+
+Mirrors ``mpisppy.phbase.PHBase`` (``mpisppy/phbase.py:176-1050``): same
+constructor and options contract (``options_check`` 726-755), same
+``Compute_Xbar`` -> ``Update_W`` -> ``convergence_diff`` -> stop test ->
+``solve_loop`` order (``iterk_loop`` 875-979), same ``Iter0`` checks
+(E1 / feasibility ``quit()``, 812-823), hooks (``pre_iter0``, ``post_iter0``,
+``post_iter0_after_sync``, ``miditer``, ``enditer``, ``enditer_after_sync``,
+``post_everything``), converger and hub (``spcomm.sync`` / ``is_converged``).
+
+Device mapping:
+  Compute_Xbar      phx_xbar (segmented per-node reduction) + ONE allreduce
+                    of the fused [sum p x | sum p x^2] buffer (RCCL on GPU)
+  Update_W          phx_update_w (W += rho (x - xbar), |x - xbar| per scenario,
+                    per-emulated-rank segment sums)
+  convergence_diff  allreduce of the per-rank sums; mean of per-rank means
+                    (phbase.py:330-343)
+  solve_loop        phx_set_ph_terms + phx_solve (batched PDHG + KKT polish)
+"""
+import math
+import time
+
+import numpy as np
+import torch
+
+from . import _native
+from .spopt import SPOpt
+from .views import ScenarioView
+from .spbase import _global_toc
+
+
+class PHBase(SPOpt):
+    def __init__(self, options, all_scenario_names, scenario_creator, scenario_denouement=None,
+                 all_nodenames=None, mpicomm=None, scenario_creator_kwargs=None, extensions=None,
+                 extension_kwargs=None, ph_converger=None, rho_setter=None, variable_probability=None,
+                 _native_lib=None, _device=None):
+        super().__init__(options, all_scenario_names, scenario_creator,
+                         scenario_denouement=scenario_denouement, all_nodenames=all_nodenames,
+                         mpicomm=mpicomm, extensions=extensions, extension_kwargs=extension_kwargs,
+                         scenario_creator_kwargs=scenario_creator_kwargs,
+                         variable_probability=variable_probability,
+                         _native_lib=_native_lib, _device=_device)
+        self.options = options
+        self.options_check()
+        self.ph_converger = ph_converger
+        self.rho_setter = rho_setter
+        self.iter0_solver_options = options["iter0_solver_options"]
+        self.iterk_solver_options = options["iterk_solver_options"]
+        self.current_solver_options = self.iter0_solver_options
+        self.convobject = None
+        self.conv = None
+        self._PHIter = 0
+        self.attach_xbars()
+        self._make_views()
+
+    # ------------------------------------------------------------ state
+    def attach_xbars(self):
+        """xbar/xsqbar per (node, slot) live on the device (phbase.py:1040-1050)."""
+        self._xbar_node.zero_()
+        self._xsqbar_node.zero_()
+
+    def attach_Ws_and_prox(self):
+        """W = 0, rho = defaultPHrho, W_on = prox_on = 0 (phbase.py:585-602)."""
+        N, S = self.batch.nonant.N, self._S
+        self._W = torch.zeros(max(N, 1) * S, dtype=torch.float64, device=self.device)
+        self._rho = torch.full((max(N, 1) * S,), float(self.options["defaultPHrho"]),
+                               dtype=torch.float64, device=self.device)
+        self.W_on = 0
+        self.prox_on = 0
+
+    def attach_PH_to_objective(self, add_duals, add_prox):
+        """The PH terms are applied by the native solver (phx_set_ph_terms);
+        linearised prox (phbase.py:628-692) is not supported."""
+        if self.options.get("linearize_proximal_terms", False):
+            raise NotImplementedError("linearize_proximal_terms is not supported by the batched engine")
+        self._attach_duals = bool(add_duals)
+        self._attach_prox = bool(add_prox)
+
+    def PH_Prep(self, attach_duals=True, attach_prox=True):
+        self.attach_Ws_and_prox()
+        self.attach_PH_to_objective(attach_duals, attach_prox)
+
+    def _make_views(self):
+        self.local_scenarios = {nm: ScenarioView(self, k, nm) for k, nm in enumerate(self.local_scenario_names)}
+        self.local_subproblems = self.local_scenarios
+
+    def options_check(self):
+        required = ["solver_name", "PHIterLimit", "defaultPHrho", "convthresh", "verbose", "display_progress"]
+        self._options_check(required, self.options)
+        if "display_timing" not in self.options:
+            self.options["display_timing"] = False
+        if "display_convergence_detail" not in self.options:
+            self.options["display_convergence_detail"] = False
+
+    # ------------------------------------------------------------ PH pieces
+    def Compute_Xbar(self, verbose=False):
+        """Per-node sum_s prob_coeff * x and * x^2, allreduced (phbase.py:27-107)."""
+        lib = self._native
+        lib.check(self._ctx, lib.xbar(self._ctx, self._tree, self._x.data_ptr(), self._pc.data_ptr(),
+                                      self._partial.data_ptr(), self._node_buf.data_ptr(), self._stream()),
+                  "xbar")
+        self.mpicomm.allreduce_(self._node_buf)
+        NNS = self.NNS
+        if NNS:
+            self._xbar_node.copy_(self._node_buf[:NNS])
+            self._xsqbar_node.copy_(self._node_buf[NNS:2 * NNS])
+        self._conv_cache = None
+        self._bump()
+        if verbose and self.cylinder_rank == 0:
+            print("xbar:", self._xbar_node.cpu().numpy())
+
+    def _update_w_and_diff(self, update):
+        lib = self._native
+        lib.check(self._ctx, lib.update_w(self._ctx, self._x.data_ptr(), self._xbar_node.data_ptr(),
+                                          self._xbar_idx_t.data_ptr(), self._rho.data_ptr(),
+                                          self._W.data_ptr(), int(update), self._dsum.data_ptr(),
+                                          self._conv_R, self._seg_s0, self._seg_s1,
+                                          self._seg_sums.data_ptr(), self._stream()), "update_w")
+        self._conv_cache = self._seg_sums.clone()
+        self._bump()
+
+    def Update_W(self, verbose):
+        """W += rho (x - xbar) (phbase.py:293-318)."""
+        self._update_w_and_diff(True)
+        if verbose and self.cylinder_rank == 0:
+            print("W:", self._W.view(-1, self._S)[:, :3].cpu().numpy())
+
+    def convergence_diff(self):
+        """(1/R) sum_r mean_{(s,i) in rank r} |x - xbar|  (phbase.py:321-343)."""
+        if getattr(self, "_conv_cache", None) is None:
+            self._update_w_and_diff(False)
+        t = self._conv_cache.clone()
+        self.mpicomm.allreduce_(t)
+        v = t.cpu().numpy()
+        cnt = self._conv_counts
+        tot = 0.0
+        for r in range(self._conv_R):
+            if cnt[r] > 0:
+                tot += v[r] / cnt[r]
+        return tot / self._conv_R
+
+    def _populate_W_cache(self, cache, padding):
+        """Flat scenario-major W export (phbase.py:346-366)."""
+        N, S = self.batch.nonant.N, self._S
+        if len(cache) - padding < N * S:
+            raise RuntimeError("W cache length mismatch detected by %s that has total W len %d but "
+                               "passed cache len-1=%d; len(nonants)=%d"
+                               % (self.__class__.__name__, N * S, len(cache) - 1, N))
+        flat = self._W.view(N, S).t().contiguous().view(-1).cpu().numpy()
+        cache[:N * S] = flat
+        assert N * S == len(cache) - padding
+
+    def W_from_flat_list(self, flat_list):
+        """Set W from a flat scenario-major list (phbase.py:369-385)."""
+        N, S = self.batch.nonant.N, self._S
+        a = torch.as_tensor(np.asarray(flat_list[:N * S], dtype=np.float64)).view(S, N).t().contiguous()
+        self._W.copy_(a.view(-1).to(self.device))
+        self._bump()
+
+    def _use_rho_setter(self, verbose):
+        """rho from a user callback returning [(id(var), rho)] (phbase.py:387-406)."""
+        if self.rho_setter is None:
+            return
+        kw = self.options.get("rho_setter_kwargs", {})
+        didit = 0
+        for sname, view in self.local_scenarios.items():
+            target = self._models[sname] if self._models is not None else view
+            for vid, rho in self.rho_setter(target, **kw):
+                j = view._slot_of_varid(vid)
+                self._host_write("rho", j, view._s, rho)
+                didit += 1
+        if verbose and self.cylinder_rank == 0:
+            print("rho_setter set", didit)
+
+    def _disable_prox(self):
+        self.prox_on = 0
+
+    def _disable_W(self):
+        self.W_on = 0
+
+    def disable_W_and_prox(self):
+        self._disable_W()
+        self._disable_prox()
+
+    def _reenable_prox(self):
+        self.prox_on = 1 if getattr(self, "_attach_prox", True) else 0
+
+    def _reenable_W(self):
+        self.W_on = 1 if getattr(self, "_attach_duals", True) else 0
+
+    def reenable_W_and_prox(self):
+        self._reenable_W()
+        self._reenable_prox()
+
+    @property
+    def W_disabled(self):
+        return not bool(self.W_on)
+
+    @property
+    def prox_disabled(self):
+        return not bool(self.prox_on)
+
+    def post_solve_bound(self, solver_options=None, verbose=False):
+        """Lagrangian bound with the current W (phbase.py:443-491)."""
+        if self.cylinder_rank == 0:
+            print("Warning: Lagrangian bounds might not be correct in certain cases where there are "
+                  "integers not subject to non-anticipativity and those integers do not reach integrality.")
+        if self.W_disabled:
+            self._reenable_W()
+        self._disable_prox()
+        self.solve_loop(solver_options=solver_options, dis_prox=False, gripe=True, tee=False, verbose=verbose)
+        bound = self.Ebound(verbose)
+        self._reenable_prox()
+        if verbose and self.cylinder_rank == 0:
+            print("Post-solve Lagrangian bound: %.4f" % bound)
+        return bound
+
+    def solve_loop(self, solver_options=None, use_scenarios_not_subproblems=False, dtiming=False,
+                   dis_W=False, dis_prox=False, gripe=False, disable_pyomo_signal_handling=False,
+                   tee=False, verbose=False):
+        """W/prox toggles around the batched solve (phbase.py:494-568)."""
+        if dis_W and dis_prox:
+            self.disable_W_and_prox()
+        elif dis_W:
+            self._disable_W()
+        elif dis_prox:
+            self._disable_prox()
+        super().solve_loop(solver_options, use_scenarios_not_subproblems, dtiming, gripe,
+                           disable_pyomo_signal_handling, tee, verbose)
+        if dis_W and dis_prox:
+            self.reenable_W_and_prox()
+        elif dis_W:
+            self._reenable_W()
+        elif dis_prox:
+            self._reenable_prox()
+
+    # ------------------------------------------------------------ loops
+    def Iter0(self):
+        """phbase.py:758-872."""
+        if self.extensions is not None:
+            self.extobject.pre_iter0()
+        verbose = self.options["verbose"]
+        dprogress = self.options["display_progress"]
+        dtiming = self.options["display_timing"]
+        have_extensions = self.extensions is not None
+        have_converger = self.ph_converger is not None
+        self._PHIter = 0
+        self._create_solvers()
+        teeme = bool(self.options.get("tee-rank0-solves", False)) and self.cylinder_rank == 0
+        self.solve_loop(solver_options=self.current_solver_options, dtiming=dtiming, gripe=True,
+                        tee=teeme, verbose=verbose)
+        self._update_E1()
+        if abs(1 - self.E1) > self.E1_tolerance:
+            if self.cylinder_rank == 0:
+                print("ERROR")
+                print("Total probability of scenarios was ", self.E1)
+                print("E1_tolerance = ", self.E1_tolerance)
+            quit()
+        feasP = self.feas_prob()
+        if feasP != self.E1:
+            if self.cylinder_rank == 0:
+                print("ERROR")
+                print("Infeasibility detected; E_feas, E1=", feasP, self.E1)
+            quit()
+        if have_extensions:
+            self.extobject.post_iter0()
+        if self.spcomm is not None:
+            self.spcomm.sync()
+        if have_extensions:
+            self.extobject.post_iter0_after_sync()
+        if self.rho_setter is not None:
+            self._use_rho_setter(verbose and self.cylinder_rank == 0)
+        if have_converger:
+            self.convobject = self.ph_converger(self)
+        self.conv = None
+        self.trivial_bound = self.Ebound(verbose)
+        if dprogress and self.cylinder_rank == 0:
+            print("")
+            print("After PH Iteration", self._PHIter)
+            print("Trivial bound =", self.trivial_bound)
+            print("PHBase Convergence Metric =", self.conv)
+            print("Elapsed time: %6.2f" % (time.perf_counter() - self.start_time))
+        if self.options["display_convergence_detail"]:
+            self.report_var_values_at_rank0(header="Convergence detail:")
+        self.reenable_W_and_prox()
+        self.current_solver_options = self.options["iterk_solver_options"]
+        return self.trivial_bound
+
+    def iterk_loop(self):
+        """phbase.py:875-979."""
+        verbose = self.options["verbose"]
+        have_extensions = self.extensions is not None
+        have_converger = self.ph_converger is not None
+        dprogress = self.options["display_progress"]
+        dtiming = self.options["display_timing"]
+        self.conv = None
+        max_iterations = int(self.options["PHIterLimit"])
+        self.iter_times = []
+        for self._PHIter in range(1, max_iterations + 1):
+            iteration_start_time = time.time()
+            if dprogress and self.cylinder_rank == 0:
+                _global_toc("Initiating PH Iteration %d" % self._PHIter)
+            self.Compute_Xbar(verbose)
+            self.Update_W(verbose)
+            self.conv = self.convergence_diff()
+            if have_extensions:
+                self.extobject.miditer()
+            if have_converger:
+                if self.convobject.is_converged():
+                    if self.cylinder_rank == 0:
+                        _global_toc("User-supplied converger determined termination criterion reached")
+                    break
+            elif self.conv is not None:
+                if self.conv < self.options["convthresh"]:
+                    if self.cylinder_rank == 0 and (dprogress or verbose):
+                        _global_toc("Convergence metric=%f dropped below user-supplied threshold=%f"
+                                    % (self.conv, self.options["convthresh"]))
+                    break
+            teeme = bool(self.options.get("tee-rank0-solves", False)) and self.cylinder_rank == 0
+            self.solve_loop(solver_options=self.current_solver_options, dtiming=dtiming, gripe=True,
+                            disable_pyomo_signal_handling=False, tee=teeme, verbose=verbose)
+            if have_extensions:
+                self.extobject.enditer()
+            if self.spcomm is not None:
+                self.spcomm.sync()
+                if self.spcomm.is_converged():
+                    if self.cylinder_rank == 0:
+                        _global_toc("Cylinder convergence")
+                    break
+            if have_extensions:
+                self.extobject.enditer_after_sync()
+            self.iter_times.append(time.time() - iteration_start_time)
+            if dprogress and self.cylinder_rank == 0:
+                print("")
+                print("After PH Iteration", self._PHIter)
+                print("Scaled PHBase Convergence Metric=", self.conv)
+                print("Iteration time: %6.2f" % (time.time() - iteration_start_time))
+                print("Elapsed time:   %6.2f" % (time.perf_counter() - self.start_time))
+            if self.options["display_convergence_detail"]:
+                self.report_var_values_at_rank0(header="Convergence detail:")
+        else:
+            self.mpicomm.Barrier()
+            if self.cylinder_rank == 0 and (dprogress or verbose):
+                _global_toc("Reached user-specified limit=%d on number of PH iterations" % max_iterations)
+
+    def post_loops(self, extensions=None):
+        """phbase.py:982-1037."""
+        verbose = self.options["verbose"]
+        have_extensions = extensions is not None
+        dprogress = self.options["display_progress"]
+        dtiming = self.options["display_timing"]
+        self.mpicomm.Barrier()
+        if self.scenario_denouement is not None:
+            for sname, s in self.local_scenarios.items():
+                target = self._models[sname] if self._models is not None else s
+                self.scenario_denouement(self.cylinder_rank, sname, target)
+        self.mpicomm.Barrier()
+        if have_extensions:
+            self.extobject.post_everything()
+        if self.ph_converger is not None and hasattr(self.ph_converger, "post_everything"):
+            self.convobject.post_everything()
+        Eobj = self.Eobjective(verbose)
+        self.mpicomm.Barrier()
+        if dprogress and self.cylinder_rank == 0:
+            print("")
+            print("Current ***weighted*** E[objective] =", Eobj)
+            print("")
+        if dtiming and self.cylinder_rank == 0:
+            print("")
+            print("Cumulative execution time=%5.2f" % (time.perf_counter() - self.start_time))
+            print("")
+        return Eobj
+
+    # ------------------------------------------------------------ accessors
+    def xbar_by_node(self):
+        """{node_name: (xbar ndarray, xsqbar ndarray)} (host copy)."""
+        xb = self._host("xbar")
+        xs = self._host("xsqbar")
+        out = {}
+        for v, nd in enumerate(self._node_names):
+            o, l = int(self._node_off[v]), int(self._node_nlen[v])
+            out[nd] = (xb[o:o + l].copy(), xs[o:o + l].copy())
+        return out
+
+    def W_array(self):
+        """(S_local, N) W values (host copy)."""
+        return self._host("W").T.copy()

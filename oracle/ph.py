@@ -1,0 +1,212 @@
+"""Oracle PH loop — TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).
+
+Plain restatement of the reference hot path, ``PH.ph_main``
+(``mpisppy/opt/ph.py:25-71``):
+
+* ``Iter0``          phbase.py:758-872 — LP solve of every scenario with
+                     W_on = prox_on = 0, trivial bound = sum_s p_s * obj_s
+                     (``Ebound`` spopt.py:346-391).
+* ``iterk_loop``     phbase.py:875-979 — per iteration:
+                     ``Compute_Xbar`` (27-107, prob_coeff = p_s / uncond_prob(node),
+                     spbase.py:378-391) -> ``Update_W`` (293-318,
+                     W += rho (x - xbar)) -> ``convergence_diff`` (321-343: mean of
+                     per-rank means of |x - xbar|) -> stop if conv < convthresh
+                     (strict, before the solve) -> solve QPs with the PH terms of
+                     ``attach_PH_to_objective`` (617-699).
+* ``post_loops``     Eobjective (spopt.py:310-343) including W and prox terms.
+
+Rank slicing for the conv normalisation follows ``_ScenTree.scen_names_to_ranks``
+(``utils/sputils.py:803-810``): rank r owns range(int(r*S/R), int((r+1)*S/R)).
+"""
+import math
+import numpy as np
+
+from . import qp
+
+
+def rank_slices(S, n_proc):
+    if n_proc == 1:
+        return [list(range(S))]
+    avg = S / n_proc
+    return [list(range(int(i * avg), int((i + 1) * avg))) for i in range(n_proc)]
+
+
+class OraclePH:
+    def __init__(self, scens, rho=1.0, n_proc=1, sense=1):
+        self.scens = scens
+        S = len(scens)
+        for s in scens:
+            if s.prob is None:
+                s.prob = 1.0 / S
+        self.S = S
+        self.n_proc = n_proc
+        self.sense = sense  # +1 min, -1 max (models here are min)
+        # nonant slots: (node_name, i) in node-list order
+        self.slots = []
+        for (ndn, cp, st, vl) in scens[0].nodes:
+            for i in range(len(vl)):
+                self.slots.append((st, i))
+        self.N = len(self.slots)
+        # per-scenario nonant columns, node names per slot, prob_coeff per slot
+        self.ncol = np.zeros((S, self.N), dtype=np.int64)
+        self.node_of = [[None] * self.N for _ in range(S)]
+        self.pc = np.zeros((S, self.N))
+        for k, s in enumerate(scens):
+            j = 0
+            uncond = 1.0
+            for (ndn, cp, st, vl) in s.nodes:
+                uncond = uncond * cp if st > 1 else 1.0
+                for v in vl:
+                    self.ncol[k, j] = v
+                    self.node_of[k][j] = ndn
+                    self.pc[k, j] = s.prob / uncond
+                    j += 1
+        self.rho = np.full((S, self.N), float(rho))
+        self.W = np.zeros((S, self.N))
+        self.xbar = np.zeros((S, self.N))
+        self.xsqbar = np.zeros((S, self.N))
+        self.x = [None] * S
+        self.obj = np.zeros(S)
+        self.W_on = 0
+        self.prox_on = 0
+        self.conv = None
+        self.iter = 0
+        self.history = []
+
+    # --- subproblem ---------------------------------------------------
+    def _qp_data(self, k):
+        s = self.scens[k]
+        q = s.c.copy()
+        p = np.zeros(len(q))
+        cols = self.ncol[k]
+        if self.W_on:
+            q[cols] += self.W[k]
+        if self.prox_on:
+            q[cols] -= self.rho[k] * self.xbar[k]
+            p[cols] += self.rho[k]
+        return q, p
+
+    def scen_objective(self, k, x):
+        s = self.scens[k]
+        f = float(np.dot(s.c, x)) + s.c0
+        xn = x[self.ncol[k]]
+        if self.W_on:
+            f += float(np.dot(self.W[k], xn))
+        if self.prox_on:
+            f += float(np.sum(self.rho[k] / 2.0 * (xn * xn - 2.0 * self.xbar[k] * xn + self.xbar[k] ** 2)))
+        return f
+
+    def solve_loop(self):
+        for k, s in enumerate(self.scens):
+            q, p = self._qp_data(k)
+            x, feas = qp.solve(s.A, s.bl, s.bu, s.lb, s.ub, q, p)
+            if not feas:
+                raise RuntimeError("oracle: infeasible scenario %s" % s.name)
+            self.x[k] = x
+            self.obj[k] = self.scen_objective(k, x)
+
+    # --- PH pieces ----------------------------------------------------
+    def xn(self):
+        return np.array([self.x[k][self.ncol[k]] for k in range(self.S)])
+
+    def compute_xbar(self):
+        xn = self.xn()
+        sums, sqs = {}, {}
+        for k in range(self.S):
+            for j in range(self.N):
+                key = (self.node_of[k][j], j)
+                sums[key] = sums.get(key, 0.0) + self.pc[k, j] * xn[k, j]
+                sqs[key] = sqs.get(key, 0.0) + self.pc[k, j] * xn[k, j] ** 2
+        for k in range(self.S):
+            for j in range(self.N):
+                key = (self.node_of[k][j], j)
+                self.xbar[k, j] = sums[key]
+                self.xsqbar[k, j] = sqs[key]
+
+    def update_w(self):
+        self.W += self.rho * (self.xn() - self.xbar)
+
+    def convergence_diff(self):
+        xn = self.xn()
+        tot = 0.0
+        for sl in rank_slices(self.S, self.n_proc):
+            d = 0.0
+            cnt = 0
+            for k in sl:
+                d += float(np.sum(np.abs(xn[k] - self.xbar[k])))
+                cnt += self.N
+            tot += d / cnt
+        return tot / self.n_proc
+
+    def Ebound(self):
+        return math.fsum(self.scens[k].prob * self.obj[k] for k in range(self.S))
+
+    def Eobjective(self):
+        return math.fsum(self.scens[k].prob * self.scen_objective(k, self.x[k]) for k in range(self.S))
+
+    def iter0(self):
+        self.iter = 0
+        self.W_on = self.prox_on = 0
+        self.solve_loop()
+        self.trivial_bound = self.Ebound()
+        self.W_on = self.prox_on = 1
+        return self.trivial_bound
+
+    def iterk(self, max_iterations, convthresh):
+        self.conv = None
+        for it in range(1, max_iterations + 1):
+            self.iter = it
+            self.compute_xbar()
+            self.update_w()
+            self.conv = self.convergence_diff()
+            self.history.append(self.conv)
+            if self.conv < convthresh:
+                return it
+            self.solve_loop()
+        return max_iterations
+
+    def ph_main(self, max_iterations, convthresh=1e-10):
+        tb = self.iter0()
+        self.iterk(max_iterations, convthresh)
+        Eobj = self.Eobjective()
+        return self.conv, Eobj, tb
+
+
+def solve_ef(scens):
+    """Extensive form (``sputils.create_EF``, utils/sputils.py:127-341) as one LP:
+    scenario blocks plus nonanticipativity equalities x_s[slot] == x_ref(node)[slot]."""
+    import scipy.sparse as sp
+    S = len(scens)
+    for s in scens:
+        if s.prob is None:
+            s.prob = 1.0 / S
+    ns = [len(s.c) for s in scens]
+    off = np.concatenate([[0], np.cumsum(ns)])
+    n = int(off[-1])
+    c = np.concatenate([s.prob * s.c for s in scens])
+    lb = np.concatenate([s.lb for s in scens])
+    ub = np.concatenate([s.ub for s in scens])
+    blocks = [s.A for s in scens]
+    A = sp.block_diag(blocks).toarray()
+    bl = np.concatenate([s.bl for s in scens])
+    bu = np.concatenate([s.bu for s in scens])
+    first = {}
+    extra = []
+    for k, s in enumerate(scens):
+        for (ndn, cp, st, vl) in s.nodes:
+            for i, v in enumerate(vl):
+                key = (ndn, i)
+                if key not in first:
+                    first[key] = off[k] + v
+                else:
+                    r = np.zeros(n)
+                    r[off[k] + v] = 1.0
+                    r[first[key]] = -1.0
+                    extra.append(r)
+    if extra:
+        A = np.vstack([A, np.array(extra)])
+        bl = np.concatenate([bl, np.zeros(len(extra))])
+        bu = np.concatenate([bu, np.zeros(len(extra))])
+    x, status = qp.highs_solve(A, bl, bu, lb, ub, c)
+    obj = float(np.dot(c, x)) + sum(s.prob * s.c0 for s in scens)
+    return obj, x, status
