@@ -39,15 +39,16 @@ def _path(sname, branching_factors):
     return nodenames
 
 
-def _demands_creator(sname, branching_factors, root_name="ROOT", **kwargs):
+def _demands_creator(sname, sample_branching_factors, root_name="ROOT", **kwargs):
     """aircond.py:37-67 (the per-node seeded demand walk)."""
     if "start_seed" not in kwargs:
         raise RuntimeError("start_seed not in kwargs=%s" % kwargs)
     start_seed = kwargs["start_seed"]
     max_d = kwargs.get("max_d", 400)
     min_d = kwargs.get("min_d", 0)
-    mu_dev = kwargs.get("mu_dev", None)
-    sigma_dev = kwargs.get("sigma_dev", None)
+    mu_dev = kwargs.get("mu_dev", parms["mu_dev"])
+    sigma_dev = kwargs.get("sigma_dev", parms["sigma_dev"])
+    branching_factors = sample_branching_factors
     nodenames = _path(sname, branching_factors)
     d = kwargs.get("starting_d", 200)
     demands = [d]
@@ -164,8 +165,8 @@ def batch_creator(scenario_names, **kwargs):
     start_seed = kwargs["start_seed"]
     max_d = kwargs.get("max_d", 400)
     min_d = kwargs.get("min_d", 0)
-    mu_dev = kwargs.get("mu_dev", None)
-    sigma_dev = kwargs.get("sigma_dev", None)
+    mu_dev = kwargs.get("mu_dev", parms["mu_dev"])
+    sigma_dev = kwargs.get("sigma_dev", parms["sigma_dev"])
     starting_d = kwargs.get("starting_d", 200)
     stream = np.random.RandomState()
     D = np.empty((S, T))
@@ -218,6 +219,14 @@ def batch_creator(scenario_names, **kwargs):
 
 
 scenario_creator.batch_creator = batch_creator
+
+
+def kw_creator(options):
+    """All model parameters with the reference defaults (aircond.py:19-35), as
+    the reference's kw_creator supplies them."""
+    kw = {k: options.get(k, v) for k, v in parms.items()}
+    kw["branching_factors"] = options.get("branching_factors")
+    return kw
 
 
 def scenario_names_creator(num_scens, start=None):

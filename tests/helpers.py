@@ -1,0 +1,35 @@
+"""Shared helpers for the parity tests (run the engine and the oracle side by side)."""
+import numpy as np
+
+import mpisppy_amd  # noqa: F401
+from mpisppy_amd.opt.ph import PH
+from oracle import models as om, ph as oph
+
+
+def ph_options(iters, rho=1.0, convthresh=1e-10, solver=None):
+    return {"solver_name": "phx", "PHIterLimit": iters, "defaultPHrho": rho, "convthresh": convthresh,
+            "verbose": False, "display_progress": False,
+            "iter0_solver_options": dict(solver or {}), "iterk_solver_options": dict(solver or {})}
+
+
+def rel(a, b):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    return float(np.max(np.abs(a - b) / np.maximum(1.0, np.abs(b)))) if a.size else 0.0
+
+
+def run_engine(creator, names, kwargs, iters, rho=1.0, lib=None, device=None, all_nodenames=None,
+               options=None, mpicomm=None):
+    opts = ph_options(iters, rho)
+    if options:
+        opts.update(options)
+    ph = PH(opts, names, creator, scenario_creator_kwargs=kwargs, all_nodenames=all_nodenames,
+            mpicomm=mpicomm, _native_lib=lib, _device=device)
+    conv, Eobj, tb = ph.ph_main()
+    return ph, conv, Eobj, tb
+
+
+REF_XBAR = np.array([96.88717449844287, 274.2239371483933, 128.88888831920772])
+REF_W = np.array([[-16.10425295139681, 70.84705093609978, -54.742797934166234],
+                  [-41.104251445950844, 89.57647412029155, -48.47222265026873],
+                  [57.20850439734766, -160.42352505639107, 103.21502058443501]])

@@ -1,0 +1,54 @@
+"""GPU parity: the real libphx kernels against the CPU oracle and the reference goldens.
+
+Tolerance (north_star): xbar, W and the PH objective within 1e-6 relative;
+every subproblem optimum polished to a KKT certificate of 1e-9.
+"""
+import numpy as np
+import pytest
+
+from helpers import REF_W, REF_XBAR, rel, run_engine
+from mpisppy_amd.examples import farmer, aircond
+from oracle import models as om, ph as oph
+
+pytestmark = pytest.mark.gpu
+
+
+def test_farmer3_golden(gpu_lib):
+    ph, conv, Eobj, tb = run_engine(farmer.scenario_creator, farmer.scenario_names_creator(3),
+                                    {"num_scens": 3}, 5, lib=gpu_lib)
+    xbar = ph.xbar_by_node()["ROOT"][0]
+    assert rel(xbar, REF_XBAR) < 1e-7
+    assert np.max(np.abs(ph.W_array() - REF_W)) < 5e-6        # reference asserts places=5
+    o = oph.OraclePH([om.farmer("scen%d" % i, num_scens=3) for i in range(3)], rho=1.0)
+    oc, oE, otb = o.ph_main(5)
+    assert rel(xbar, o.xbar[0]) < 1e-9
+    assert rel(ph.W_array(), o.W) < 1e-8
+    assert rel(Eobj, oE) < 1e-9 and rel(tb, otb) < 1e-9 and rel(conv, oc) < 1e-7
+
+
+@pytest.mark.parametrize("S", [30, 300])
+def test_farmer_many_vs_oracle(gpu_lib, S):
+    ph, conv, Eobj, tb = run_engine(farmer.scenario_creator, farmer.scenario_names_creator(S),
+                                    {"num_scens": S}, 3, lib=gpu_lib)
+    o = oph.OraclePH([om.farmer("scen%d" % i, num_scens=S) for i in range(S)], rho=1.0)
+    oc, oE, otb = o.ph_main(3)
+    assert rel(tb, otb) < 1e-9
+    assert rel(ph.xbar_by_node()["ROOT"][0], o.xbar[0]) < 1e-8
+    assert rel(ph.W_array(), o.W) < 1e-7
+    assert rel(Eobj, oE) < 1e-8
+    assert all(s["not_optimal"] == 0 for s in ph.solve_stats)
+
+
+def test_aircond_multistage_vs_oracle(gpu_lib):
+    bfs = [3, 3, 2]
+    from mpisppy_amd.utils import sputils
+    names = ["scen%d" % i for i in range(18)]
+    ph, conv, Eobj, tb = run_engine(aircond.scenario_creator, names, {"branching_factors": bfs, "start_seed": 0},
+                                    4, lib=gpu_lib,
+                                    all_nodenames=sputils.create_nodenames_from_branching_factors(bfs))
+    scens = [om.aircond(n, bfs, start_seed=0) for n in names]
+    o = oph.OraclePH(scens, rho=1.0)
+    oc, oE, otb = o.ph_main(4)
+    assert rel(tb, otb) < 1e-9
+    assert rel(Eobj, oE) < 1e-8
+    assert rel(ph.W_array(), o.W) < 1e-7
