@@ -73,6 +73,11 @@ typedef struct phx_solve_opts {
     double  opt_tol;          /* accept unpolished point when rel. KKT < this */
     double  kkt_tol;          /* polish certificate tolerance (relative)      */
     double  reg;              /* polish regularisation (scaled units)         */
+    int32_t ipm_after;        /* PDHG iterations after which a lane still not
+                                 certified switches to the interior-point
+                                 finisher (0: IPM first; <0: never)           */
+    int32_t ipm_max_it;       /* IPM iteration cap                            */
+    double  ipm_tol;          /* IPM relative KKT target                      */
 } phx_solve_opts;
 
 /* Scenario-tree reduction layout for Compute_Xbar (phbase.py:27-107): for each
@@ -171,10 +176,10 @@ int phx_export_slots(phx_ctx* ctx, const double* src, double* out, void* stream)
 /* Timing of the most recent phx_solve: summed kernel milliseconds of the PDHG
  * chunk launches (HIP events on the solve stream), their count, the
  * scenario-iterations they performed (sum over launches of running lanes x
- * check_every) and the polish milliseconds.                                */
+ * check_every), the polish and the interior-point-finisher milliseconds. */
 int phx_last_solve_timing(const phx_ctx* ctx, double* pdhg_ms_host,
                           int32_t* pdhg_launches_host, double* lane_iters_host,
-                          double* polish_ms_host);
+                          double* polish_ms_host, double* ipm_ms_host);
 
 #ifdef __cplusplus
 }

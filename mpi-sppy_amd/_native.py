@@ -38,6 +38,7 @@ class SolveOpts(ctypes.Structure):
         ("polish", c_int32), ("refine_steps", c_int32), ("warm_start", c_int32),
         ("polish_below", c_double), ("opt_tol", c_double), ("kkt_tol", c_double),
         ("reg", c_double),
+        ("ipm_after", c_int32), ("ipm_max_it", c_int32), ("ipm_tol", c_double),
     ]
 
 
@@ -101,7 +102,7 @@ class Lib:
         self.expect = fn("expect", ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p])
         self.export_slots = fn("export_slots", ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p])
         self.last_solve_timing = fn("last_solve_timing", ctypes.c_int,
-                                    [c_void_p, P_f64, P_i32, P_f64, P_f64])
+                                    [c_void_p, P_f64, P_i32, P_f64, P_f64, P_f64])
 
     def check(self, ctx, rc, what):
         if rc != 0:

@@ -60,6 +60,7 @@ struct State {
     double *x, *y, *x0, *y0, *xT, *yT, *xb;  // scaled iterates [n|m][S]
     double *omega, *eta, *r0, *rprev, *err;  // [S]
     int32_t *hk, *status, *iters;            // [S]
+    int32_t *flags;                          // [S] bit0: interior-point finisher tried
 };
 
 struct Opts {
@@ -72,6 +73,9 @@ struct Opts {
     int32_t refine_steps;
     int32_t polish;
     int32_t max_iters;
+    int32_t ipm_after;    // PDHG iterations before a lane switches to the IPM finisher (<0: never)
+    int32_t ipm_max_it;
+    double ipm_tol;
 };
 
 struct Polish {   // polish workspace, all [.][S]
@@ -84,6 +88,12 @@ struct Polish {   // polish workspace, all [.][S]
     double* brhs; // [m]  active row right-hand side
     unsigned char* F;  // [n] 1 = free column
     unsigned char* R;  // [m] 1 = active row
+};
+
+struct Ipm {      // interior-point finisher workspace, all [.][S]
+    double *s, *zl, *zu, *wl, *wu;            // row activity, bound multipliers
+    double *dx, *dzl, *dzu, *cl, *cu, *hx;    // [n]
+    double *ds, *dwl, *dwu, *dy, *cwl, *cwu;  // [m]
 };
 
 PHX_HD int64_t ix(int i, int s, int S) { return (int64_t)i * S + s; }
@@ -264,14 +274,23 @@ PHX_HD bool polish_lane(const Prob& P, const State& St, const Polish& W, const O
     const int S = P.S, n = P.n, m = P.m;
     const double reg = O.reg;
     // ---- classify ----
+    // A bound/row is active when its slack is within tol (relative), or when
+    // its slack is smaller than its correctly-signed multiplier (OSQP's
+    // polish rule, sharp at interior-point points by strict complementarity).
     for (int j = 0; j < n; ++j) {
         const int64_t o = ix(j, s, S);
         const double x = St.xT[o];
         const double l = P.lb.at(j, s), u = P.ub.at(j, s);
+        double aty = 0.0;
+        for (int k = P.colptr[j]; k < P.colptr[j + 1]; ++k)
+            aty += aval(P, P.csc2csr[k], s) * St.yT[ix(P.rowidx[k], s, S)];
+        double q, p;
+        col_cost(P, j, s, q, p);
+        const double lam = q + p * x - aty;
         unsigned char f = 1;
         double xf = 0.0;
-        if (isfinite(l) && x - l <= tol * (1.0 + fabs(l))) { f = 0; xf = l; }
-        else if (isfinite(u) && u - x <= tol * (1.0 + fabs(u))) { f = 0; xf = u; }
+        if (isfinite(l) && (x - l <= tol * (1.0 + fabs(l)) || x - l < lam)) { f = 0; xf = l; }
+        else if (isfinite(u) && (u - x <= tol * (1.0 + fabs(u)) || u - x < -lam)) { f = 0; xf = u; }
         W.F[o] = f;
         W.xfix[o] = xf;
         W.xp[o] = f ? x : xf;
@@ -284,8 +303,9 @@ PHX_HD bool polish_lane(const Prob& P, const State& St, const Polish& W, const O
         const int64_t o = ix(i, s, S);
         unsigned char r = 0;
         double b = 0.0;
-        if (isfinite(bl) && ax - bl <= tol * (1.0 + fabs(bl))) { r = 1; b = bl; }
-        else if (isfinite(bu) && bu - ax <= tol * (1.0 + fabs(bu))) { r = 1; b = bu; }
+        const double yv = St.yT[o];
+        if (isfinite(bl) && (ax - bl <= tol * (1.0 + fabs(bl)) || ax - bl < yv)) { r = 1; b = bl; }
+        else if (isfinite(bu) && (bu - ax <= tol * (1.0 + fabs(bu)) || bu - ax < -yv)) { r = 1; b = bu; }
         W.R[o] = r;
         W.brhs[o] = b;
         W.z[o] = r ? -St.yT[o] : 0.0;
@@ -436,6 +456,343 @@ PHX_HD bool polish_lane(const Prob& P, const State& St, const Polish& W, const O
     return true;
 }
 
+// ---------------------------------------------------------------------------
+// Interior-point finisher (Mehrotra predictor-corrector), one lane per
+// scenario, for lanes PDHG has not certified.  Problem (scaled space):
+//   min 0.5 x'Px + q'x  s.t.  A x - s = 0,  l <= x <= u,  bl <= s <= bu
+// with bound multipliers z_l, z_u (columns) and w_l, w_u (rows); equality rows
+// carry no slack, free rows keep y = 0.  Newton systems reduce to the m x m
+// normal matrix  M = A (P + Sigma_x)^-1 A' + Sigma_s^-1,  factored in place with
+// the same packed, scenario-minor Cholesky as the polish.  The iterate lands
+// in St.xT / St.yT (y > 0 <=> lower side active, the PDHG convention) so the
+// polish certifies it.  Returns the final relative KKT error.
+// ---------------------------------------------------------------------------
+PHX_HD bool ipm_fixed(double l, double u) { return l == u; }
+
+PHX_HD double ipm_mu(const Prob& P, const State& St, const Ipm& I, int s, int& ncomp) {
+    const int S = P.S;
+    double acc = 0.0;
+    ncomp = 0;
+    for (int j = 0; j < P.n; ++j) {
+        const int64_t o = ix(j, s, S);
+        const double l = P.lb.at(j, s), u = P.ub.at(j, s), x = St.xT[o];
+        if (ipm_fixed(l, u)) continue;
+        if (isfinite(l)) { acc += (x - l) * I.zl[o]; ++ncomp; }
+        if (isfinite(u)) { acc += (u - x) * I.zu[o]; ++ncomp; }
+    }
+    for (int i = 0; i < P.m; ++i) {
+        const int64_t o = ix(i, s, S);
+        const double bl = P.bl.at(i, s), bu = P.bu.at(i, s), sv = I.s[o];
+        if (bl == bu) continue;
+        if (isfinite(bl)) { acc += (sv - bl) * I.wl[o]; ++ncomp; }
+        if (isfinite(bu)) { acc += (bu - sv) * I.wu[o]; ++ncomp; }
+    }
+    return ncomp ? acc / ncomp : 0.0;
+}
+
+// Solve the Newton system for given complementarity targets (cl, cu, cwl, cwu
+// already in I); M must hold the Cholesky factor.  Writes the direction.
+PHX_HD void ipm_direction(const Prob& P, const State& St, const Polish& W, const Ipm& I, int s) {
+    const int S = P.S, n = P.n, m = P.m;
+    // rho_x -> I.dx (temporarily), rho_s -> I.ds (temporarily)
+    for (int j = 0; j < n; ++j) {
+        const int64_t o = ix(j, s, S);
+        const double l = P.lb.at(j, s), u = P.ub.at(j, s), x = St.xT[o];
+        if (ipm_fixed(l, u)) { I.dx[o] = 0.0; continue; }
+        double aty = 0.0;
+        for (int k = P.colptr[j]; k < P.colptr[j + 1]; ++k)
+            aty += aval(P, P.csc2csr[k], s) * St.yT[ix(P.rowidx[k], s, S)];
+        double q, p;
+        col_cost(P, j, s, q, p);
+        double rd = p * x + q - aty;
+        double rho = 0.0;
+        if (isfinite(l)) { rd -= I.zl[o]; rho += I.cl[o] / (x - l); }
+        if (isfinite(u)) { rd += I.zu[o]; rho -= I.cu[o] / (u - x); }
+        I.dx[o] = rho - rd;
+    }
+    for (int i = 0; i < m; ++i) {
+        const int64_t o = ix(i, s, S);
+        const double bl = P.bl.at(i, s), bu = P.bu.at(i, s);
+        double ax = 0.0;
+        for (int k = P.rowptr[i]; k < P.rowptr[i + 1]; ++k)
+            ax += aval(P, k, s) * St.xT[ix(P.colidx[k], s, S)];
+        double adr = 0.0;   // (A H^-1 rho_x)_i
+        for (int k = P.rowptr[i]; k < P.rowptr[i + 1]; ++k) {
+            const int64_t oj = ix(P.colidx[k], s, S);
+            adr += aval(P, k, s) * I.dx[oj] / I.hx[oj];
+        }
+        double rhs;
+        if (!isfinite(bl) && !isfinite(bu)) {
+            rhs = 0.0;                      // free row: y stays 0
+            I.ds[o] = 0.0;
+        } else if (bl == bu) {
+            rhs = -(ax - bl) - adr;
+            I.ds[o] = 0.0;
+        } else {
+            const double sv = I.s[o];
+            const double y = St.yT[o];
+            double rs = y, rhos = 0.0, sig = 0.0;
+            if (isfinite(bl)) { rs -= I.wl[o]; rhos += I.cwl[o] / (sv - bl); sig += I.wl[o] / (sv - bl); }
+            if (isfinite(bu)) { rs += I.wu[o]; rhos -= I.cwu[o] / (bu - sv); sig += I.wu[o] / (bu - sv); }
+            rhos -= rs;
+            I.ds[o] = rhos;                 // rho_s kept for the back-substitution
+            rhs = -(ax - sv) + rhos / sig - adr;
+        }
+        W.t[o] = rhs;
+    }
+    // dy = M^-1 rhs
+    for (int i = 0; i < m; ++i) {
+        double v = W.t[ix(i, s, S)];
+        for (int k = 0; k < i; ++k) v -= W.L[ix((int)tri(i, k), s, S)] * W.t[ix(k, s, S)];
+        W.t[ix(i, s, S)] = v / W.L[ix((int)tri(i, i), s, S)];
+    }
+    for (int i = m - 1; i >= 0; --i) {
+        double v = W.t[ix(i, s, S)];
+        for (int k = i + 1; k < m; ++k) v -= W.L[ix((int)tri(k, i), s, S)] * W.t[ix(k, s, S)];
+        W.t[ix(i, s, S)] = v / W.L[ix((int)tri(i, i), s, S)];
+    }
+    for (int i = 0; i < m; ++i) {
+        const int64_t o = ix(i, s, S);
+        const double bl = P.bl.at(i, s), bu = P.bu.at(i, s);
+        const double dy = W.t[o];
+        I.dy[o] = dy;
+        if (isfinite(bl) && isfinite(bu) && bl == bu) continue;
+        if (!isfinite(bl) && !isfinite(bu)) continue;
+        const double sv = I.s[o];
+        double sig = 0.0;
+        if (isfinite(bl)) sig += I.wl[o] / (sv - bl);
+        if (isfinite(bu)) sig += I.wu[o] / (bu - sv);
+        const double dsv = (I.ds[o] - dy) / sig;
+        I.ds[o] = dsv;
+        if (isfinite(bl)) I.dwl[o] = (I.cwl[o] - I.wl[o] * dsv) / (sv - bl);
+        if (isfinite(bu)) I.dwu[o] = (I.cwu[o] + I.wu[o] * dsv) / (bu - sv);
+    }
+    for (int j = 0; j < n; ++j) {
+        const int64_t o = ix(j, s, S);
+        const double l = P.lb.at(j, s), u = P.ub.at(j, s), x = St.xT[o];
+        if (ipm_fixed(l, u)) { I.dx[o] = 0.0; continue; }
+        double atdy = 0.0;
+        for (int k = P.colptr[j]; k < P.colptr[j + 1]; ++k)
+            atdy += aval(P, P.csc2csr[k], s) * I.dy[ix(P.rowidx[k], s, S)];
+        const double dxv = (I.dx[o] + atdy) / I.hx[o];
+        I.dx[o] = dxv;
+        if (isfinite(l)) I.dzl[o] = (I.cl[o] - I.zl[o] * dxv) / (x - l);
+        if (isfinite(u)) I.dzu[o] = (I.cu[o] + I.zu[o] * dxv) / (u - x);
+    }
+}
+
+PHX_HD void ipm_steps(const Prob& P, const State& St, const Ipm& I, int s, double& ap, double& ad) {
+    const int S = P.S;
+    ap = 1.0;
+    ad = 1.0;
+    for (int j = 0; j < P.n; ++j) {
+        const int64_t o = ix(j, s, S);
+        const double l = P.lb.at(j, s), u = P.ub.at(j, s), x = St.xT[o], d = I.dx[o];
+        if (ipm_fixed(l, u)) continue;
+        if (isfinite(l)) {
+            if (d < 0.0) ap = fmin(ap, -(x - l) / d);
+            if (I.dzl[o] < 0.0) ad = fmin(ad, -I.zl[o] / I.dzl[o]);
+        }
+        if (isfinite(u)) {
+            if (d > 0.0) ap = fmin(ap, (u - x) / d);
+            if (I.dzu[o] < 0.0) ad = fmin(ad, -I.zu[o] / I.dzu[o]);
+        }
+    }
+    for (int i = 0; i < P.m; ++i) {
+        const int64_t o = ix(i, s, S);
+        const double bl = P.bl.at(i, s), bu = P.bu.at(i, s), sv = I.s[o], d = I.ds[o];
+        if (bl == bu) continue;
+        if (isfinite(bl)) {
+            if (d < 0.0) ap = fmin(ap, -(sv - bl) / d);
+            if (I.dwl[o] < 0.0) ad = fmin(ad, -I.wl[o] / I.dwl[o]);
+        }
+        if (isfinite(bu)) {
+            if (d > 0.0) ap = fmin(ap, (bu - sv) / d);
+            if (I.dwu[o] < 0.0) ad = fmin(ad, -I.wu[o] / I.dwu[o]);
+        }
+    }
+}
+
+PHX_HD double ipm_lane(const Prob& P, const State& St, const Polish& W, const Ipm& I, int s,
+                       int max_it, double tol, double reg) {
+    const int S = P.S, n = P.n, m = P.m;
+    // ---- start point ----
+    for (int j = 0; j < n; ++j) {
+        const int64_t o = ix(j, s, S);
+        const double l = P.lb.at(j, s), u = P.ub.at(j, s);
+        double x;
+        if (ipm_fixed(l, u)) x = l;
+        else if (isfinite(l) && isfinite(u)) x = (u - l <= 2.0) ? 0.5 * (l + u) : clampd(0.0, l + 1.0, u - 1.0);
+        else x = clampd(0.0, isfinite(l) ? l + 1.0 : -1e300, isfinite(u) ? u - 1.0 : 1e300);
+        St.xT[o] = x;
+        // cost-aware start: bound multipliers absorb the linear cost so the
+        // initial dual residual is O(1) even with costs spanning 1e1..1e5
+        double q, p;
+        col_cost(P, j, s, q, p);
+        const double g = q + p * x;
+        I.zl[o] = isfinite(l) && !ipm_fixed(l, u) ? fmax(g, 0.0) + 1.0 : 0.0;
+        I.zu[o] = isfinite(u) && !ipm_fixed(l, u) ? fmax(-g, 0.0) + 1.0 : 0.0;
+        I.dzl[o] = I.dzu[o] = 0.0;
+    }
+    for (int i = 0; i < m; ++i) {
+        const int64_t o = ix(i, s, S);
+        const double bl = P.bl.at(i, s), bu = P.bu.at(i, s);
+        double ax = 0.0;
+        for (int k = P.rowptr[i]; k < P.rowptr[i + 1]; ++k)
+            ax += aval(P, k, s) * St.xT[ix(P.colidx[k], s, S)];
+        double sv = ax;
+        const bool eq = (bl == bu);
+        if (eq) sv = bl;
+        else if (isfinite(bl) && isfinite(bu)) sv = (bu - bl <= 2.0) ? 0.5 * (bl + bu) : clampd(ax, bl + 1.0, bu - 1.0);
+        else sv = clampd(ax, isfinite(bl) ? bl + 1.0 : -1e300, isfinite(bu) ? bu - 1.0 : 1e300);
+        I.s[o] = sv;
+        I.wl[o] = (isfinite(bl) && !eq) ? 1.0 : 0.0;
+        I.wu[o] = (isfinite(bu) && !eq) ? 1.0 : 0.0;
+        I.dwl[o] = I.dwu[o] = 0.0;
+        St.yT[o] = I.wl[o] - I.wu[o];
+    }
+    double err = 1e300;
+    for (int it = 0; it < max_it; ++it) {
+        err = kkt_error(P, St.xT, St.yT, s);
+        int ncomp;
+        const double mu = ipm_mu(P, St, I, s, ncomp);
+#if defined(PHX_IPM_TRACE)
+        if (s == PHX_IPM_TRACE) printf("[ipm s=%d] it=%d err=%.3e mu=%.3e\n", s, it, err, mu);
+#endif
+        if (err < tol || !(err < 1e300)) break;
+        // ---- H_x, normal matrix, Cholesky ----
+        for (int j = 0; j < n; ++j) {
+            const int64_t o = ix(j, s, S);
+            const double l = P.lb.at(j, s), u = P.ub.at(j, s), x = St.xT[o];
+            double q, p;
+            col_cost(P, j, s, q, p);
+            double h = p + reg;
+            if (ipm_fixed(l, u)) h = 1e300;
+            else {
+                if (isfinite(l)) h += I.zl[o] / (x - l);
+                if (isfinite(u)) h += I.zu[o] / (u - x);
+            }
+            I.hx[o] = h;
+        }
+        for (int i = 0; i < m; ++i) {
+            const double bl = P.bl.at(i, s), bu = P.bu.at(i, s);
+            const int64_t o = ix(i, s, S);
+            double dg;
+            if (!isfinite(bl) && !isfinite(bu)) dg = 1.0;
+            else if (bl == bu) dg = reg;
+            else {
+                const double sv = I.s[o];
+                double sig = 0.0;
+                if (isfinite(bl)) sig += I.wl[o] / (sv - bl);
+                if (isfinite(bu)) sig += I.wu[o] / (bu - sv);
+                dg = 1.0 / sig + reg;
+            }
+            for (int k = 0; k < i; ++k) W.L[ix((int)tri(i, k), s, S)] = 0.0;
+            W.L[ix((int)tri(i, i), s, S)] = dg;
+        }
+        for (int j = 0; j < n; ++j) {
+            const double D = 1.0 / I.hx[ix(j, s, S)];
+            for (int ka = P.colptr[j]; ka < P.colptr[j + 1]; ++ka) {
+                const int ia = P.rowidx[ka];
+                const double bla = P.bl.at(ia, s), bua = P.bu.at(ia, s);
+                if (!isfinite(bla) && !isfinite(bua)) continue;
+                const double va = aval(P, P.csc2csr[ka], s) * D;
+                for (int kb = P.colptr[j]; kb <= ka; ++kb) {
+                    const int ib = P.rowidx[kb];
+                    const double blb = P.bl.at(ib, s), bub = P.bu.at(ib, s);
+                    if (!isfinite(blb) && !isfinite(bub)) continue;
+                    const int hi = ia > ib ? ia : ib, lo = ia > ib ? ib : ia;
+                    W.L[ix((int)tri(hi, lo), s, S)] += va * aval(P, P.csc2csr[kb], s);
+                }
+            }
+        }
+        bool okc = true;
+        for (int jj = 0; jj < m && okc; ++jj) {
+            double d = W.L[ix((int)tri(jj, jj), s, S)];
+            for (int k = 0; k < jj; ++k) {
+                const double v = W.L[ix((int)tri(jj, k), s, S)];
+                d -= v * v;
+            }
+            if (!(d > 0.0)) { okc = false; break; }
+            d = sqrt(d);
+            W.L[ix((int)tri(jj, jj), s, S)] = d;
+            for (int i = jj + 1; i < m; ++i) {
+                double v = W.L[ix((int)tri(i, jj), s, S)];
+                for (int k = 0; k < jj; ++k)
+                    v -= W.L[ix((int)tri(i, k), s, S)] * W.L[ix((int)tri(jj, k), s, S)];
+                W.L[ix((int)tri(i, jj), s, S)] = v / d;
+            }
+        }
+        if (!okc) break;
+        // ---- predictor ----
+        for (int j = 0; j < n; ++j) {
+            const int64_t o = ix(j, s, S);
+            const double l = P.lb.at(j, s), u = P.ub.at(j, s), x = St.xT[o];
+            I.cl[o] = isfinite(l) ? -(x - l) * I.zl[o] : 0.0;
+            I.cu[o] = isfinite(u) ? -(u - x) * I.zu[o] : 0.0;
+        }
+        for (int i = 0; i < m; ++i) {
+            const int64_t o = ix(i, s, S);
+            const double bl = P.bl.at(i, s), bu = P.bu.at(i, s), sv = I.s[o];
+            I.cwl[o] = (isfinite(bl) && bl != bu) ? -(sv - bl) * I.wl[o] : 0.0;
+            I.cwu[o] = (isfinite(bu) && bl != bu) ? -(bu - sv) * I.wu[o] : 0.0;
+        }
+        ipm_direction(P, St, W, I, s);
+        double ap, ad;
+        ipm_steps(P, St, I, s, ap, ad);
+        // affine complementarity
+        double maff = 0.0;
+        for (int j = 0; j < n; ++j) {
+            const int64_t o = ix(j, s, S);
+            const double l = P.lb.at(j, s), u = P.ub.at(j, s), x = St.xT[o];
+            if (ipm_fixed(l, u)) continue;
+            if (isfinite(l)) maff += (x - l + ap * I.dx[o]) * (I.zl[o] + ad * I.dzl[o]);
+            if (isfinite(u)) maff += (u - x - ap * I.dx[o]) * (I.zu[o] + ad * I.dzu[o]);
+        }
+        for (int i = 0; i < m; ++i) {
+            const int64_t o = ix(i, s, S);
+            const double bl = P.bl.at(i, s), bu = P.bu.at(i, s), sv = I.s[o];
+            if (bl == bu) continue;
+            if (isfinite(bl)) maff += (sv - bl + ap * I.ds[o]) * (I.wl[o] + ad * I.dwl[o]);
+            if (isfinite(bu)) maff += (bu - sv - ap * I.ds[o]) * (I.wu[o] + ad * I.dwu[o]);
+        }
+        maff = ncomp ? maff / ncomp : 0.0;
+        const double ratio = mu > 0.0 ? maff / mu : 0.0;
+        const double smu = ratio * ratio * ratio * mu;
+        // ---- corrector ----
+        for (int j = 0; j < n; ++j) {
+            const int64_t o = ix(j, s, S);
+            const double l = P.lb.at(j, s), u = P.ub.at(j, s), x = St.xT[o];
+            I.cl[o] = isfinite(l) ? smu - (x - l) * I.zl[o] - I.dx[o] * I.dzl[o] : 0.0;
+            I.cu[o] = isfinite(u) ? smu - (u - x) * I.zu[o] + I.dx[o] * I.dzu[o] : 0.0;
+        }
+        for (int i = 0; i < m; ++i) {
+            const int64_t o = ix(i, s, S);
+            const double bl = P.bl.at(i, s), bu = P.bu.at(i, s), sv = I.s[o];
+            I.cwl[o] = (isfinite(bl) && bl != bu) ? smu - (sv - bl) * I.wl[o] - I.ds[o] * I.dwl[o] : 0.0;
+            I.cwu[o] = (isfinite(bu) && bl != bu) ? smu - (bu - sv) * I.wu[o] + I.ds[o] * I.dwu[o] : 0.0;
+        }
+        ipm_direction(P, St, W, I, s);
+        ipm_steps(P, St, I, s, ap, ad);
+        ap = fmin(1.0, 0.995 * ap);
+        ad = fmin(1.0, 0.995 * ad);
+        for (int j = 0; j < n; ++j) {
+            const int64_t o = ix(j, s, S);
+            St.xT[o] += ap * I.dx[o];
+            I.zl[o] += ad * I.dzl[o];
+            I.zu[o] += ad * I.dzu[o];
+        }
+        for (int i = 0; i < m; ++i) {
+            const int64_t o = ix(i, s, S);
+            I.s[o] += ap * I.ds[o];
+            I.wl[o] += ad * I.dwl[o];
+            I.wu[o] += ad * I.dwu[o];
+            St.yT[o] += ad * I.dy[o];
+        }
+    }
+    return err;
+}
+
 // After a successful polish: adopt the polished point as the solution and as
 // the warm start for the next solve.
 PHX_HD void adopt_polished(const Prob& P, const State& St, const Polish& W, int s) {
@@ -450,6 +807,36 @@ PHX_HD void adopt_polished(const Prob& P, const State& St, const Polish& W, int 
         const double v = -W.z[o];
         St.yT[o] = v; St.y[o] = v; St.y0[o] = v;
     }
+}
+
+// IPM finisher for one lane + polish; returns true when the lane is done.
+PHX_HD bool finish_lane(const Prob& P, const State& St, const Polish& W, const Ipm& I, const Opts& O,
+                        int s) {
+    St.flags[s] |= 1;
+    const double e = ipm_lane(P, St, W, I, s, O.ipm_max_it, O.ipm_tol, 1e-10);
+    St.err[s] = e;
+    bool done = false;
+    if (e < 1e-4 && O.polish) {
+        const double tol = fmin(1e-4, fmax(1e-9, 10.0 * e));
+        if (polish_lane(P, St, W, O, s, tol)) {
+            adopt_polished(P, St, W, s);
+            done = true;
+        }
+    }
+    if (!done && e < O.opt_tol) done = true;
+    // warm start / restart PDHG from the IPM point either way
+    for (int j = 0; j < P.n; ++j) {
+        const int64_t o = ix(j, s, P.S);
+        St.x[o] = St.x0[o] = St.xT[o];
+    }
+    for (int i = 0; i < P.m; ++i) {
+        const int64_t o = ix(i, s, P.S);
+        St.y[o] = St.y0[o] = St.yT[o];
+    }
+    St.hk[s] = 0;
+    St.r0[s] = 1e301;
+    St.rprev[s] = 1e301;
+    return done;
 }
 
 // Unscaled outputs + objective (c'x + qN'x_N + 0.5 pN x_N^2 + kN), the value

@@ -29,9 +29,13 @@ using namespace phx;
 #define PHX_BLOCK 64   // lane-per-scenario kernels: one wavefront per block
 
 // ------------------------------------------------------------------ kernels
-__global__ __launch_bounds__(PHX_BLOCK) void k_chunk(Prob P, State St, Opts O) {
-    const int s = blockIdx.x * PHX_BLOCK + threadIdx.x;
-    if (s >= P.S) return;
+// Lane lists: launches cover only still-running scenarios.  lanes[0..*count)
+// holds scenario ids (ascending within a wavefront), rebuilt by k_polish.
+__global__ __launch_bounds__(PHX_BLOCK) void k_chunk(Prob P, State St, Opts O, const int32_t* lanes,
+                                                    const int32_t* count) {
+    const int t = blockIdx.x * PHX_BLOCK + threadIdx.x;
+    if (t >= *count) return;
+    const int s = lanes[t];
     if (St.status[s] != RUNNING) return;
     int hk = St.hk[s];
     const double eta = St.eta[s];
@@ -50,11 +54,24 @@ __global__ __launch_bounds__(PHX_BLOCK) void k_chunk(Prob P, State St, Opts O) {
     if (!(e < 1e300)) St.status[s] = NUMERIC_FAIL;
 }
 
+// Interior-point finisher for lanes that PDHG has not certified after
+// O.ipm_after iterations (O.ipm_after = 0: IPM first), followed by the polish.
+__global__ __launch_bounds__(PHX_BLOCK) void k_ipm(Prob P, State St, Polish W, Ipm I, Opts O,
+                                                  const int32_t* lanes, const int32_t* count) {
+    const int t = blockIdx.x * PHX_BLOCK + threadIdx.x;
+    if (t >= *count) return;
+    const int s = lanes[t];
+    if (St.status[s] != RUNNING || St.iters[s] < O.ipm_after || (St.flags[s] & 1)) return;
+    if (finish_lane(P, St, W, I, O, s)) St.status[s] = OPTIMAL;
+}
+
 __global__ __launch_bounds__(PHX_BLOCK) void k_polish(Prob P, State St, Polish W, Opts O,
-                                                     int32_t* running) {
-    const int s = blockIdx.x * PHX_BLOCK + threadIdx.x;
+                                                     const int32_t* lanes, const int32_t* count,
+                                                     int32_t* lanes_out, int32_t* running) {
+    const int t = blockIdx.x * PHX_BLOCK + threadIdx.x;
+    const int s = t < *count ? lanes[t] : -1;
     bool still = false;
-    if (s < P.S && St.status[s] == RUNNING) {
+    if (s >= 0 && St.status[s] == RUNNING) {
         const double e = St.err[s];
         if (O.polish && e < O.polish_below) {
             const double tol = fmin(1e-4, fmax(1e-9, 10.0 * e));
@@ -68,9 +85,22 @@ __global__ __launch_bounds__(PHX_BLOCK) void k_polish(Prob P, State St, Polish W
             else still = true;
         }
     }
-    // one atomic per wavefront
+    // compact the still-running lanes: one atomic per wavefront, lane order kept
     const unsigned long long b = __ballot(still);
-    if ((threadIdx.x & 63) == 0 && b) atomicAdd(running, (int32_t)__popcll(b));
+    const int lane = threadIdx.x & 63;
+    int base = 0;
+    if (lane == 0 && b) base = atomicAdd(running, (int32_t)__popcll(b));
+    base = __shfl(base, 0, 64);
+    if (still) {
+        const unsigned long long below = b & ((1ull << lane) - 1ull);
+        lanes_out[base + __popcll(below)] = s;
+    }
+}
+
+__global__ void k_iota(int32_t* lanes, int32_t* count, int S) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < S) lanes[t] = t;
+    if (t == 0) *count = S;
 }
 
 __global__ __launch_bounds__(PHX_BLOCK) void k_finalize(Prob P, State St, const double* c,
@@ -123,6 +153,7 @@ __global__ void k_begin_solve(Prob P, State St, int warm) {
     St.status[s] = RUNNING;
     St.iters[s] = 0;
     St.err[s] = 1e300;
+    St.flags[s] = 0;
 }
 
 __global__ void k_norm(Prob P, State St, int iters) {
@@ -306,17 +337,23 @@ struct phx_ctx {
     double *bls = nullptr, *bus = nullptr, *dr = nullptr, *dc = nullptr;
     double *qN = nullptr, *pN = nullptr, *kN = nullptr;
     int32_t* running = nullptr;
+    int32_t* lanesA = nullptr;
+    int32_t* lanesB = nullptr;
+    int32_t* countA = nullptr;
     int32_t* running_host = nullptr;
     Prob P{};
     State St{};
     Polish Pw{};
+    Ipm Iw{};
+    bool have_ipm = false;
     // tree/seg caches
     std::vector<int32_t> seg_s0_cache, seg_s1_cache;
     int32_t *seg_ts0 = nullptr, *seg_ts1 = nullptr, *seg_ptr = nullptr;
     double* seg_part = nullptr;
     int seg_ntiles = 0;
     // timing
-    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr, ev4 = nullptr;
+    double last_ipm_ms = 0.0;
     double last_pdhg_ms = 0.0, last_polish_ms = 0.0;
     int32_t last_launches = 0;
     double last_lane_iters = 0.0;
@@ -327,6 +364,8 @@ struct phx_ctx {
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
         if (ev2) (void)hipEventDestroy(ev2);
+        if (ev3) (void)hipEventDestroy(ev3);
+        if (ev4) (void)hipEventDestroy(ev4);
     }
     template <class T> T* alloc(size_t count) {
         void* p = nullptr;
@@ -371,6 +410,8 @@ int phx_create(int32_t device, phx_ctx** out) {
     (void)hipEventCreate(&c->ev0);
     (void)hipEventCreate(&c->ev1);
     (void)hipEventCreate(&c->ev2);
+    (void)hipEventCreate(&c->ev3);
+    (void)hipEventCreate(&c->ev4);
     *out = c;
     return 0;
 }
@@ -444,6 +485,9 @@ int phx_set_problem(phx_ctx* ctx, const phx_problem_desc* d) {
     ctx->pN = ctx->alloc<double>((size_t)N * S);
     ctx->kN = ctx->alloc<double>(S);
     ctx->running = ctx->alloc<int32_t>(1);
+    ctx->lanesA = ctx->alloc<int32_t>(S);
+    ctx->lanesB = ctx->alloc<int32_t>(S);
+    ctx->countA = ctx->alloc<int32_t>(1);
     PHX_REQUIRE(ctx, ctx->running && ctx->kN && ctx->bus, "phx_set_problem: out of device memory");
     PHX_CHECK(ctx, hipMemcpy(ctx->colptr, colptr.data(), sizeof(int32_t) * (n + 1), hipMemcpyHostToDevice));
     if (nnz) {
@@ -515,12 +559,24 @@ int phx_set_problem(phx_ctx* ctx, const phx_problem_desc* d) {
     St.omega = ctx->alloc<double>(S); St.eta = ctx->alloc<double>(S); St.r0 = ctx->alloc<double>(S);
     St.rprev = ctx->alloc<double>(S); St.err = ctx->alloc<double>(S);
     St.hk = ctx->alloc<int32_t>(S); St.status = ctx->alloc<int32_t>(S); St.iters = ctx->alloc<int32_t>(S);
+    St.flags = ctx->alloc<int32_t>(S);
     Polish& W = ctx->Pw;
     W.L = ctx->alloc<double>((size_t)m * (m + 1) / 2 * S);
     W.z = ctx->alloc<double>(mS); W.r1 = ctx->alloc<double>(nS); W.t = ctx->alloc<double>(mS);
     W.xp = ctx->alloc<double>(nS); W.xfix = ctx->alloc<double>(nS); W.brhs = ctx->alloc<double>(mS);
     W.F = ctx->alloc<unsigned char>(nS); W.R = ctx->alloc<unsigned char>(mS);
-    PHX_REQUIRE(ctx, St.x && St.iters && W.L && W.R, "phx_set_problem: out of device memory (state)");
+    PHX_REQUIRE(ctx, St.x && St.iters && St.flags && W.L && W.R, "phx_set_problem: out of device memory (state)");
+    {
+        Ipm& I = ctx->Iw;
+        I.s = ctx->alloc<double>(mS); I.zl = ctx->alloc<double>(nS); I.zu = ctx->alloc<double>(nS);
+        I.wl = ctx->alloc<double>(mS); I.wu = ctx->alloc<double>(mS);
+        I.dx = ctx->alloc<double>(nS); I.dzl = ctx->alloc<double>(nS); I.dzu = ctx->alloc<double>(nS);
+        I.cl = ctx->alloc<double>(nS); I.cu = ctx->alloc<double>(nS); I.hx = ctx->alloc<double>(nS);
+        I.ds = ctx->alloc<double>(mS); I.dwl = ctx->alloc<double>(mS); I.dwu = ctx->alloc<double>(mS);
+        I.dy = ctx->alloc<double>(mS); I.cwl = ctx->alloc<double>(mS); I.cwu = ctx->alloc<double>(mS);
+        ctx->have_ipm = I.cwu != nullptr;
+        PHX_REQUIRE(ctx, ctx->have_ipm, "phx_set_problem: out of device memory (ipm)");
+    }
     hipLaunchKernelGGL(k_norm, dim3(nblk(S, PHX_BLOCK)), dim3(PHX_BLOCK), 0, 0, P, St, 100);
     hipLaunchKernelGGL(k_begin_solve, dim3(nblk(S, PHX_BLOCK)), dim3(PHX_BLOCK), 0, 0, P, St, 0);
     PHX_CHECK(ctx, hipGetLastError());
@@ -561,34 +617,58 @@ int phx_solve(phx_ctx* ctx, const phx_solve_opts* o, double* x_out, double* y_ou
     O.refine_steps = o->refine_steps;
     O.polish = o->polish;
     O.max_iters = o->max_iters;
+    O.ipm_after = o->ipm_after;
+    O.ipm_max_it = o->ipm_max_it;
+    O.ipm_tol = o->ipm_tol;
     const int warm = (o->warm_start && ctx->solved_once) ? 1 : 0;
     hipLaunchKernelGGL(k_begin_solve, dim3(G), dim3(PHX_BLOCK), 0, st, ctx->P, ctx->St, warm);
     PHX_CHECK(ctx, hipGetLastError());
     int total = 0;
     int running = S;
-    double pdhg_ms = 0.0, polish_ms = 0.0, lane_iters = 0.0;
+    bool ipm_done = false, ipm_launched = false;
+    double pdhg_ms = 0.0, polish_ms = 0.0, lane_iters = 0.0, ipm_ms = 0.0;
     int launches = 0;
+    hipLaunchKernelGGL(k_iota, dim3(nblk(S, 256)), dim3(256), 0, st, ctx->lanesA, ctx->countA, S);
+    int32_t* lin = ctx->lanesA;
+    int32_t* lout = ctx->lanesB;
+    int32_t* cin = ctx->countA;
+    int32_t* cout = ctx->running;
     while (running > 0 && total < o->max_iters) {
-        PHX_CHECK(ctx, hipMemsetAsync(ctx->running, 0, sizeof(int32_t), st));
+        const unsigned Gr = nblk(running, PHX_BLOCK);
+        PHX_CHECK(ctx, hipMemsetAsync(cout, 0, sizeof(int32_t), st));
+        if (O.ipm_after >= 0 && total >= O.ipm_after && !ipm_done) {
+            PHX_CHECK(ctx, hipEventRecord(ctx->ev3, st));
+            hipLaunchKernelGGL(k_ipm, dim3(Gr), dim3(PHX_BLOCK), 0, st, ctx->P, ctx->St, ctx->Pw, ctx->Iw, O,
+                               lin, cin);
+            PHX_CHECK(ctx, hipEventRecord(ctx->ev4, st));
+            ipm_done = true;
+            ipm_launched = true;
+        }
         PHX_CHECK(ctx, hipEventRecord(ctx->ev0, st));
-        hipLaunchKernelGGL(k_chunk, dim3(G), dim3(PHX_BLOCK), 0, st, ctx->P, ctx->St, O);
+        hipLaunchKernelGGL(k_chunk, dim3(Gr), dim3(PHX_BLOCK), 0, st, ctx->P, ctx->St, O, lin, cin);
         PHX_CHECK(ctx, hipEventRecord(ctx->ev1, st));
-        hipLaunchKernelGGL(k_polish, dim3(G), dim3(PHX_BLOCK), 0, st, ctx->P, ctx->St, ctx->Pw, O,
-                           ctx->running);
+        hipLaunchKernelGGL(k_polish, dim3(Gr), dim3(PHX_BLOCK), 0, st, ctx->P, ctx->St, ctx->Pw, O, lin, cin,
+                           lout, cout);
         PHX_CHECK(ctx, hipEventRecord(ctx->ev2, st));
         PHX_CHECK(ctx, hipGetLastError());
-        PHX_CHECK(ctx, hipMemcpyAsync(ctx->running_host, ctx->running, sizeof(int32_t),
-                                      hipMemcpyDeviceToHost, st));
+        PHX_CHECK(ctx, hipMemcpyAsync(ctx->running_host, cout, sizeof(int32_t), hipMemcpyDeviceToHost, st));
         PHX_CHECK(ctx, hipStreamSynchronize(st));
-        float a = 0.f, b = 0.f;
+        float a = 0.f, b = 0.f, c = 0.f;
         (void)hipEventElapsedTime(&a, ctx->ev0, ctx->ev1);
         (void)hipEventElapsedTime(&b, ctx->ev1, ctx->ev2);
+        if (ipm_launched) {
+            (void)hipEventElapsedTime(&c, ctx->ev3, ctx->ev4);
+            ipm_ms += c;
+            ipm_launched = false;
+        }
         pdhg_ms += a;
         polish_ms += b;
         lane_iters += (double)running * o->check_every;
         ++launches;
         total += o->check_every;
         running = *ctx->running_host;
+        std::swap(lin, lout);
+        std::swap(cin, cout);
     }
     const int64_t c_si = ctx->c_vary ? S : 1, c_ss = ctx->c_vary ? 1 : 0;
     hipLaunchKernelGGL(k_finalize, dim3(G), dim3(PHX_BLOCK), 0, st, ctx->P, ctx->St, ctx->c_user, c_si,
@@ -599,6 +679,7 @@ int phx_solve(phx_ctx* ctx, const phx_solve_opts* o, double* x_out, double* y_ou
     ctx->last_polish_ms = polish_ms;
     ctx->last_launches = launches;
     ctx->last_lane_iters = lane_iters;
+    ctx->last_ipm_ms = ipm_ms;
     if (total_iters_host) *total_iters_host = total;
     return 0;
 }
@@ -690,12 +771,13 @@ int phx_export_slots(phx_ctx* ctx, const double* src, double* out, void* stream)
 }
 
 int phx_last_solve_timing(const phx_ctx* ctx, double* pdhg_ms, int32_t* launches, double* lane_iters,
-                          double* polish_ms) {
+                          double* polish_ms, double* ipm_ms) {
     if (!ctx) return 1;
     if (pdhg_ms) *pdhg_ms = ctx->last_pdhg_ms;
     if (launches) *launches = ctx->last_launches;
     if (lane_iters) *lane_iters = ctx->last_lane_iters;
     if (polish_ms) *polish_ms = ctx->last_polish_ms;
+    if (ipm_ms) *ipm_ms = ctx->last_ipm_ms;
     return 0;
 }
 

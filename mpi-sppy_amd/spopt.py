@@ -12,7 +12,8 @@ Solver knobs come from the ``solver_options`` dict exactly where the reference
 passes solver options (``iter0_solver_options`` / ``iterk_solver_options``,
 phbase.py:273-275): keys ``pdhg_max_iters``, ``pdhg_check_every``,
 ``pdhg_restart_max``, ``polish``, ``polish_refine``, ``polish_below``,
-``kkt_tol``, ``opt_tol``, ``polish_reg``, ``warm_start``.
+``kkt_tol``, ``opt_tol``, ``polish_reg``, ``warm_start``, ``ipm_after``,
+``ipm_max_it``, ``ipm_tol``.
 """
 import ctypes
 import inspect
@@ -35,6 +36,9 @@ SOLVER_DEFAULTS = {
     "kkt_tol": 1e-9,
     "polish_reg": 1e-6,
     "warm_start": 1,
+    "ipm_after": 1024,
+    "ipm_max_it": 60,
+    "ipm_tol": 1e-10,
 }
 
 OPTIMAL, ITER_LIMIT, NUMERIC_FAIL = 1, 2, 3
@@ -87,6 +91,9 @@ class SPOpt(SPBase):
         so.opt_tol = float(o["opt_tol"])
         so.kkt_tol = float(o["kkt_tol"])
         so.reg = float(o["polish_reg"])
+        so.ipm_after = int(o["ipm_after"])
+        so.ipm_max_it = int(o["ipm_max_it"])
+        so.ipm_tol = float(o["ipm_tol"])
         return so
 
     def _set_ph_terms(self):
@@ -123,12 +130,14 @@ class SPOpt(SPBase):
         pms = ctypes.c_double(0)
         la = ctypes.c_int32(0)
         li = ctypes.c_double(0)
+        ims = ctypes.c_double(0)
         lib.check(self._ctx, lib.last_solve_timing(self._ctx, ctypes.byref(ms), ctypes.byref(la),
-                                                   ctypes.byref(li), ctypes.byref(pms)), "last_solve_timing")
+                                                   ctypes.byref(li), ctypes.byref(pms), ctypes.byref(ims)),
+                  "last_solve_timing")
         st = self._status
         n_bad = int((st != OPTIMAL).sum().item())
         self.solve_stats.append({"pdhg_iters": int(total.value), "pdhg_ms": ms.value, "launches": la.value,
-                                 "lane_iters": li.value, "polish_ms": pms.value,
+                                 "lane_iters": li.value, "polish_ms": pms.value, "ipm_ms": ims.value,
                                  "wall_s": time.perf_counter() - t0, "not_optimal": n_bad})
         if n_bad and gripe:
             stc = st.cpu().numpy()

@@ -15,6 +15,8 @@
 #include <string>
 #include <vector>
 #include <algorithm>
+#include <stdio.h>
+#include <stdlib.h>
 #include "../../include/phx.h"
 #include "../../mpi-sppy_amd/csrc/phx_core.h"
 #include "../../mpi-sppy_amd/csrc/phx_setup.h"
@@ -29,7 +31,9 @@ struct emu_ctx {
     HostSetup hs;
     std::vector<double> Av, cs, lbs, ubs, bls, bus, qN, pN, kN, c_user;
     std::vector<double> x, y, x0, y0, xT, yT, xb, omega, eta, r0, rprev, errv;
-    std::vector<int32_t> hk, status, iters;
+    std::vector<int32_t> hk, status, iters, flags;
+    std::vector<double> ipm_buf;
+    Ipm Iw{};
     std::vector<double> L, z, r1, t, xp, xfix, brhs;
     std::vector<unsigned char> F, R;
     Prob P{};
@@ -111,7 +115,7 @@ int emu_phx_set_problem(emu_ctx* c, const phx_problem_desc* d) {
     for (auto* v : {&c->x, &c->x0, &c->xT, &c->xb, &c->r1, &c->xp, &c->xfix}) v->assign(nS, 0.0);
     for (auto* v : {&c->y, &c->y0, &c->yT, &c->z, &c->t, &c->brhs}) v->assign(mS, 0.0);
     for (auto* v : {&c->omega, &c->eta, &c->r0, &c->rprev, &c->errv}) v->assign(S, 0.0);
-    c->hk.assign(S, 0); c->status.assign(S, 0); c->iters.assign(S, 0);
+    c->hk.assign(S, 0); c->status.assign(S, 0); c->iters.assign(S, 0); c->flags.assign(S, 0);
     c->L.assign((size_t)m * (m + 1) / 2 * S + 1, 0.0);
     c->F.assign(nS, 0); c->R.assign(mS, 0);
     State& St = c->St;
@@ -119,6 +123,16 @@ int emu_phx_set_problem(emu_ctx* c, const phx_problem_desc* d) {
     St.xT = c->xT.data(); St.yT = c->yT.data(); St.xb = c->xb.data();
     St.omega = c->omega.data(); St.eta = c->eta.data(); St.r0 = c->r0.data(); St.rprev = c->rprev.data();
     St.err = c->errv.data(); St.hk = c->hk.data(); St.status = c->status.data(); St.iters = c->iters.data();
+    St.flags = c->flags.data();
+    c->ipm_buf.assign((size_t)(8 * n + 9 * std::max(m, 1)) * S, 0.0);
+    {
+        double* b = c->ipm_buf.data();
+        auto take = [&](size_t k) { double* r = b; b += k; return r; };
+        Ipm& I = c->Iw;
+        I.s = take(mS); I.zl = take(nS); I.zu = take(nS); I.wl = take(mS); I.wu = take(mS);
+        I.dx = take(nS); I.dzl = take(nS); I.dzu = take(nS); I.cl = take(nS); I.cu = take(nS); I.hx = take(nS);
+        I.ds = take(mS); I.dwl = take(mS); I.dwu = take(mS); I.dy = take(mS); I.cwl = take(mS); I.cwu = take(mS);
+    }
     Polish& W = c->Pw;
     W.L = c->L.data(); W.z = c->z.data(); W.r1 = c->r1.data(); W.t = c->t.data(); W.xp = c->xp.data();
     W.xfix = c->xfix.data(); W.brhs = c->brhs.data(); W.F = c->F.data(); W.R = c->R.data();
@@ -168,6 +182,7 @@ int emu_phx_solve(emu_ctx* c, const phx_solve_opts* o, double* x_out, double* y_
     O.iters = o->check_every; O.restart_max = o->restart_max; O.polish_below = o->polish_below;
     O.opt_tol = o->opt_tol; O.kkt_tol = o->kkt_tol; O.reg = o->reg; O.refine_steps = o->refine_steps;
     O.polish = o->polish; O.max_iters = o->max_iters;
+    O.ipm_after = o->ipm_after; O.ipm_max_it = o->ipm_max_it; O.ipm_tol = o->ipm_tol;
     const bool warm = o->warm_start && c->solved_once;
     for (int s = 0; s < S; ++s) {
         if (!warm) {
@@ -182,6 +197,7 @@ int emu_phx_solve(emu_ctx* c, const phx_solve_opts* o, double* x_out, double* y_
         }
         St.hk[s] = 0; St.r0[s] = 1e301; St.rprev[s] = 1e301; St.status[s] = RUNNING; St.iters[s] = 0;
         St.err[s] = 1e300;
+        St.flags[s] = 0;
     }
     int total = 0, running = S;
     c->lane_iters = 0;
@@ -192,6 +208,9 @@ int emu_phx_solve(emu_ctx* c, const phx_solve_opts* o, double* x_out, double* y_
         running = 0;
         for (int s = 0; s < S; ++s) {
             if (St.status[s] != RUNNING) continue;
+            if (O.ipm_after >= 0 && St.iters[s] >= O.ipm_after && !(St.flags[s] & 1)) {
+                if (finish_lane(P, St, c->Pw, c->Iw, O, s)) { St.status[s] = OPTIMAL; continue; }
+            }
             int hk = St.hk[s];
             const double tau = St.eta[s] / St.omega[s], sigma = St.eta[s] * St.omega[s];
             double dx2 = 0, dy2 = 0;
@@ -205,13 +224,20 @@ int emu_phx_solve(emu_ctx* c, const phx_solve_opts* o, double* x_out, double* y_
             const double e = St.err[s];
             if (!O.polish && e < O.opt_tol) St.status[s] = OPTIMAL;
             if (!(e < 1e300)) St.status[s] = NUMERIC_FAIL;
+            bool tried = false, okp = false;
             if (St.status[s] == RUNNING && O.polish && e < O.polish_below) {
                 const double tol = fmin(1e-4, fmax(1e-9, 10.0 * e));
+                tried = true;
                 if (polish_lane(P, St, c->Pw, O, s, tol)) {
                     adopt_polished(P, St, c->Pw, s);
                     St.status[s] = OPTIMAL;
+                    okp = true;
                 }
             }
+            static int trace_s = getenv("PHX_EMU_TRACE") ? atoi(getenv("PHX_EMU_TRACE")) : -1;
+            if (s == trace_s)
+                fprintf(stderr, "[emu s=%d] it=%d err=%.3e omega=%.3e hk=%d r0=%.3e polish=%s\n", s, St.iters[s], e,
+                        St.omega[s], St.hk[s], St.r0[s], tried ? (okp ? "OK" : "fail") : "-");
             if (St.status[s] == RUNNING) {
                 if (St.iters[s] >= O.max_iters) St.status[s] = ITER_LIMIT;
                 else ++running;
@@ -312,7 +338,8 @@ int emu_phx_export_slots(emu_ctx* c, const double* src, double* out, void*) {
 }
 
 int emu_phx_last_solve_timing(const emu_ctx* c, double* ms, int32_t* launches, double* lane_iters,
-                              double* pms) {
+                              double* pms, double* ims) {
+    if (ims) *ims = 0;
     if (ms) *ms = 0;
     if (launches) *launches = c->launches;
     if (lane_iters) *lane_iters = c->lane_iters;

@@ -1,0 +1,74 @@
+"""N>1 path on CPU: two gloo ranks (one 'GPU' each) give the same PH result as
+one process; the fused allreduce replaces the per-node MPI reductions."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out, case):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import mpisppy_amd  # noqa: F401
+    from mpisppy_amd import _native
+    from mpisppy_amd.comm import Comm
+    from helpers import run_engine
+    from mpisppy_amd.examples import aircond, farmer
+    from mpisppy_amd.utils import sputils
+    emu = _native.Lib(os.path.join(ROOT, "tests", "emu", "libphx_emu.so"), prefix="emu_phx_")
+    if case == "farmer":
+        ph, conv, Eobj, tb = run_engine(farmer.scenario_creator, farmer.scenario_names_creator(9),
+                                        {"num_scens": 9}, 4, lib=emu, device="cpu", mpicomm=Comm())
+    else:
+        bfs = [3, 2, 2]
+        ph, conv, Eobj, tb = run_engine(aircond.scenario_creator, ["scen%d" % i for i in range(12)],
+                                        {"branching_factors": bfs, "start_seed": 0}, 3, lib=emu, device="cpu",
+                                        mpicomm=Comm(),
+                                        all_nodenames=sputils.create_nodenames_from_branching_factors(bfs))
+    out[rank] = (conv, Eobj, tb, ph.W_array(), {k: v[0] for k, v in ph.xbar_by_node().items()})
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case", ["farmer", "aircond"])
+def test_two_ranks_match_one(emu, case):
+    from helpers import run_engine
+    from mpisppy_amd.examples import aircond, farmer
+    from mpisppy_amd.utils import sputils
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(2, _free_port(), out, case), nprocs=2, join=True)
+    if case == "farmer":
+        ph, conv, Eobj, tb = run_engine(farmer.scenario_creator, farmer.scenario_names_creator(9), {"num_scens": 9},
+                                        4, lib=emu, device="cpu", options={"conv_ranks": 2})
+    else:
+        bfs = [3, 2, 2]
+        ph, conv, Eobj, tb = run_engine(aircond.scenario_creator, ["scen%d" % i for i in range(12)],
+                                        {"branching_factors": bfs, "start_seed": 0}, 3, lib=emu, device="cpu",
+                                        options={"conv_ranks": 2},
+                                        all_nodenames=sputils.create_nodenames_from_branching_factors(bfs))
+    r0, r1 = out[0], out[1]
+    for r in (r0, r1):
+        assert r[0] == pytest.approx(conv, rel=1e-12)
+        assert r[1] == pytest.approx(Eobj, rel=1e-12)
+        assert r[2] == pytest.approx(tb, rel=1e-12)
+        for k, v in ph.xbar_by_node().items():
+            assert np.allclose(r[4][k], v[0], rtol=1e-12, atol=1e-12)
+    W = np.vstack([r0[3], r1[3]])
+    assert np.allclose(W, ph.W_array(), rtol=1e-10, atol=1e-9)

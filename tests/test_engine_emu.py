@@ -1,0 +1,138 @@
+"""The full PH engine (PHBase/PH API) on CPU through the test emulation of the
+C ABI (same per-lane solver math as the HIP kernels), against the oracle and
+the reference goldens.  The GPU versions of these checks are in test_gpu_parity.py."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from helpers import REF_W, REF_XBAR, rel, run_engine
+from mpisppy_amd.examples import aircond, farmer
+from mpisppy_amd.utils import sputils
+from oracle import models as om, ph as oph
+
+MODES = [{"ipm_after": 0}, {"ipm_after": 256}, {"ipm_after": -1}]
+
+
+@pytest.fixture(scope="module")
+def oracle_farmer30():
+    o = oph.OraclePH([om.farmer("scen%d" % i, num_scens=30) for i in range(30)], rho=1.0)
+    res = o.ph_main(4)
+    return o, res
+
+
+def test_farmer3_golden_emu(emu):
+    ph, conv, Eobj, tb = run_engine(farmer.scenario_creator, farmer.scenario_names_creator(3), {"num_scens": 3},
+                                    5, lib=emu, device="cpu")
+    assert rel(ph.xbar_by_node()["ROOT"][0], REF_XBAR) < 1e-7
+    assert np.max(np.abs(ph.W_array() - REF_W)) < 5e-6
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_farmer30_modes_vs_oracle(emu, oracle_farmer30, mode):
+    o, (oc, oE, otb) = oracle_farmer30
+    opts = {"iter0_solver_options": mode, "iterk_solver_options": mode}
+    ph, conv, Eobj, tb = run_engine(farmer.scenario_creator, farmer.scenario_names_creator(30), {"num_scens": 30},
+                                    4, lib=emu, device="cpu", options=opts)
+    assert rel(tb, otb) < 1e-9
+    assert rel(ph.xbar_by_node()["ROOT"][0], o.xbar[0]) < 1e-9
+    assert rel(ph.W_array(), o.W) < 1e-8
+    assert rel(Eobj, oE) < 1e-9
+    assert rel(conv, oc) < 1e-8
+    assert all(s["not_optimal"] == 0 for s in ph.solve_stats)
+
+
+def test_per_scenario_models_equal_batch(emu):
+    a = run_engine(farmer.scenario_creator, farmer.scenario_names_creator(12), {"num_scens": 12}, 3,
+                   lib=emu, device="cpu")
+    b = run_engine(farmer.scenario_creator, farmer.scenario_names_creator(12), {"num_scens": 12}, 3,
+                   lib=emu, device="cpu", options={"per_scenario_models": True})
+    assert np.array_equal(a[0].W_array(), b[0].W_array())
+    assert a[1:] == b[1:]
+
+
+def test_aircond_multistage_emu(emu):
+    bfs = [3, 3, 2]
+    names = ["scen%d" % i for i in range(18)]
+    ph, conv, Eobj, tb = run_engine(aircond.scenario_creator, names, {"branching_factors": bfs, "start_seed": 0},
+                                    4, lib=emu, device="cpu",
+                                    all_nodenames=sputils.create_nodenames_from_branching_factors(bfs))
+    o = oph.OraclePH([om.aircond(n, bfs, start_seed=0) for n in names], rho=1.0)
+    oc, oE, otb = o.ph_main(4)
+    assert rel(tb, otb) < 1e-12
+    assert rel(Eobj, oE) < 1e-10
+    assert rel(ph.W_array(), o.W) < 1e-10
+    # per-node xbar: 1 ROOT + 3 stage-2 + 9 stage-3 nodes
+    xb = ph.xbar_by_node()
+    assert len(xb) == 13
+    assert rel(xb["ROOT"][0], o.xbar[0, 0:2]) < 1e-12
+
+
+def test_docs_farmer_via_engine(emu):
+    """doc/src/examples.rst trajectory (rho 10, 5 iterations) through the engine."""
+    from mpisppy_amd import model as lm
+    from mpisppy_amd.utils import sputils as su
+
+    def build_model(yields):
+        m = lm.LinearModel()
+        X = m.add_indexed_var("X", ["WHEAT", "CORN", "BEETS"], lb=0.0)
+        Y = m.add_indexed_var("Y", ["WHEAT", "CORN"], lb=0.0)
+        W = m.add_indexed_var("W", ["WHEAT", "CORN", "BEETS_FAVORABLE", "BEETS_UNFAVORABLE"], lb=0.0)
+        plant = 150 * X["WHEAT"] + 230 * X["CORN"] + 260 * X["BEETS"]
+        m.set_objective(plant + 238 * Y["WHEAT"] + 210 * Y["CORN"] - 170 * W["WHEAT"] - 150 * W["CORN"]
+                        - 36 * W["BEETS_FAVORABLE"] - 10 * W["BEETS_UNFAVORABLE"])
+        m.add_constraint(X["WHEAT"] + X["CORN"] + X["BEETS"], ub=500)
+        m.add_constraint(yields[0] * X["WHEAT"] + Y["WHEAT"] - W["WHEAT"], lb=200)
+        m.add_constraint(yields[1] * X["CORN"] + Y["CORN"] - W["CORN"], lb=240)
+        m.add_constraint(yields[2] * X["BEETS"] - W["BEETS_FAVORABLE"] - W["BEETS_UNFAVORABLE"], lb=0)
+        W["BEETS_FAVORABLE"].ub = 6000
+        return m, plant, X
+
+    def scenario_creator(name):
+        y = {"good": [3, 3.6, 24], "average": [2.5, 3, 20], "bad": [2, 2.4, 16]}[name]
+        m, plant, X = build_model(y)
+        su.attach_root_node(m, plant, [X])
+        m._mpisppy_probability = 1.0 / 3
+        return m
+
+    ph, conv, Eobj, tb = run_engine(scenario_creator, ["good", "average", "bad"], None, 5, rho=10.0,
+                                    lib=emu, device="cpu")
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "ref_goldens.json")))
+    vals = ph.gather_var_values_to_rank0()
+    for sn, ref in g["docs_farmer_rho10_5iters"]["x"].items():
+        for vn, v in ref.items():
+            assert vals[sn, vn] == pytest.approx(v, rel=1e-9)
+
+
+def test_maximize_sense(emu):
+    """max problems: PH term subtracted (phbase.py:696-699); same x, negated objective."""
+    from mpisppy_amd import model as lm
+    a = run_engine(farmer.scenario_creator, farmer.scenario_names_creator(6), {"num_scens": 6}, 3,
+                   lib=emu, device="cpu")
+    b = run_engine(farmer.scenario_creator, farmer.scenario_names_creator(6),
+                   {"num_scens": 6, "sense": lm.maximize}, 3, lib=emu, device="cpu")
+    assert rel(a[0].W_array(), -b[0].W_array()) < 1e-9 or rel(a[0].nonant_values(), b[0].nonant_values()) < 1e-9
+    assert rel(a[3], -b[3]) < 1e-12           # trivial bound
+    assert rel(a[2], -b[2]) < 1e-9            # Eobj
+    assert rel(a[0].nonant_values(), b[0].nonant_values()) < 1e-9
+
+
+def test_conv_emulated_ranks(emu):
+    """options['conv_ranks'] reproduces the reference's per-rank-mean conv for R ranks."""
+    S = 10
+    o = oph.OraclePH([om.farmer("scen%d" % i, num_scens=S) for i in range(S)], rho=1.0, n_proc=3)
+    oc, oE, otb = o.ph_main(2)
+    ph, conv, Eobj, tb = run_engine(farmer.scenario_creator, farmer.scenario_names_creator(S), {"num_scens": S},
+                                    2, lib=emu, device="cpu", options={"conv_ranks": 3})
+    assert rel(conv, oc) < 1e-9
+
+
+def test_convthresh_stops_before_solve(emu):
+    """Stop test is strict and happens before the iteration's solve (phbase.py:930-934)."""
+    ph, conv, Eobj, tb = run_engine(farmer.scenario_creator, farmer.scenario_names_creator(3), {"num_scens": 3},
+                                    500, lib=emu, device="cpu", options={"convthresh": 1e-4})
+    o = oph.OraclePH([om.farmer("scen%d" % i, num_scens=3) for i in range(3)], rho=1.0)
+    it = o.iterk(500, 1e-4) if o.iter0() is not None else None
+    assert ph._PHIter == it
+    assert conv < 1e-4
