@@ -43,6 +43,7 @@ def parse():
     ap.add_argument("--rho", type=float, default=1.0)
     ap.add_argument("--check-every", type=int, default=64)
     ap.add_argument("--ipm-after", type=int, default=None, help="PDHG iterations before the IPM finisher")
+    ap.add_argument("--lane-solver", type=int, default=1, help="1: structure-specialised lane IPM first")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=400)
     ap.add_argument("--conv", action="store_true", help="also measure time to conv < 1e-4")
@@ -97,7 +98,7 @@ def main():
 
     S = args.scens
     names = farmer.scenario_names_creator(S)
-    solver_opts = {"pdhg_check_every": args.check_every}
+    solver_opts = {"pdhg_check_every": args.check_every, "lane_solver": args.lane_solver}
     if args.ipm_after is not None:
         solver_opts["ipm_after"] = args.ipm_after
     opts = {"solver_name": "phx", "PHIterLimit": 10 ** 9, "defaultPHrho": args.rho, "convthresh": 1e-10,
@@ -169,7 +170,10 @@ def main():
                      "scenario_iters_per_launch": lane_iters / max(launches, 1)},
         "pdhg_iters_per_step": [s["pdhg_iters"] for s in stats],
         "kernel_ms_per_step": {"pdhg": pdhg_ms / args.steps, "polish": sum(s["polish_ms"] for s in stats) / args.steps,
-                               "ipm": sum(s["ipm_ms"] for s in stats) / args.steps},
+                               "ipm": sum(s["ipm_ms"] for s in stats) / args.steps,
+                               "lane_ipm": sum(s.get("lane_ms", 0.0) for s in stats) / args.steps,
+                               "lane_polish": sum(s.get("lane_polish_ms", 0.0) for s in stats) / args.steps},
+        "lane_certified_per_step": [s.get("lane_certified") for s in stats],
         "solver_options": solver_opts,
         "not_optimal": sum(s["not_optimal"] for s in stats),
         "setup_s": t_setup, "iter0_s": t_iter0,

@@ -78,7 +78,24 @@ typedef struct phx_solve_opts {
                                  finisher (0: IPM first; <0: never)           */
     int32_t ipm_max_it;       /* IPM iteration cap                            */
     double  ipm_tol;          /* IPM relative KKT target                      */
+    int32_t lane_solver;      /* 1: run the register-resident, structure-
+                                 specialised lane solver (IPM + polish) first
+                                 when the context has one (small subproblems) */
 } phx_solve_opts;
+
+/* Statistics of the most recent phx_solve (HIP events on the solve stream). */
+typedef struct phx_solve_stats {
+    double  pdhg_ms;          /* summed k_chunk (PDHG) kernel time            */
+    double  polish_ms;        /* summed k_polish time                         */
+    double  ipm_ms;           /* generic interior-point finisher              */
+    double  lane_ms;          /* specialised lane IPM kernel                  */
+    double  lane_polish_ms;   /* specialised lane polish kernel               */
+    double  lane_iters;       /* PDHG scenario-iterations executed            */
+    int32_t pdhg_launches;
+    int32_t total_iters;      /* PDHG iterations of the batch loop            */
+    int32_t lane_certified;   /* scenarios certified by the lane solver       */
+    int32_t jit;              /* 1 if this context has a specialised kernel   */
+} phx_solve_stats;
 
 /* Scenario-tree reduction layout for Compute_Xbar (phbase.py:27-107): for each
  * tile, the nonant slots [slot_lo, slot_lo+nlen) of one tree node summed over
@@ -173,13 +190,11 @@ int phx_expect(phx_ctx* ctx, const double* prob, const double* obj,
  * PHHub.send_nonants (phbase.py:346-366, hub.py:562-577).                  */
 int phx_export_slots(phx_ctx* ctx, const double* src, double* out, void* stream);
 
-/* Timing of the most recent phx_solve: summed kernel milliseconds of the PDHG
- * chunk launches (HIP events on the solve stream), their count, the
- * scenario-iterations they performed (sum over launches of running lanes x
- * check_every), the polish and the interior-point-finisher milliseconds. */
-int phx_last_solve_timing(const phx_ctx* ctx, double* pdhg_ms_host,
-                          int32_t* pdhg_launches_host, double* lane_iters_host,
-                          double* polish_ms_host, double* ipm_ms_host);
+int phx_last_solve_stats(const phx_ctx* ctx, phx_solve_stats* out_host);
+
+/* Human-readable state of the structure-specialised lane solver for this
+ * context ("on: ..." or "off: <reason>").                                   */
+const char* phx_jit_info(const phx_ctx* ctx);
 
 #ifdef __cplusplus
 }

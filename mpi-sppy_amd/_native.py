@@ -39,6 +39,16 @@ class SolveOpts(ctypes.Structure):
         ("polish_below", c_double), ("opt_tol", c_double), ("kkt_tol", c_double),
         ("reg", c_double),
         ("ipm_after", c_int32), ("ipm_max_it", c_int32), ("ipm_tol", c_double),
+        ("lane_solver", c_int32),
+    ]
+
+
+class SolveStats(ctypes.Structure):
+    _fields_ = [
+        ("pdhg_ms", c_double), ("polish_ms", c_double), ("ipm_ms", c_double), ("lane_ms", c_double),
+        ("lane_polish_ms", c_double),
+        ("lane_iters", c_double), ("pdhg_launches", c_int32), ("total_iters", c_int32),
+        ("lane_certified", c_int32), ("jit", c_int32),
     ]
 
 
@@ -56,7 +66,7 @@ class TreeDesc(ctypes.Structure):
 # every symbol of include/phx.h (tests check the library exports all of them)
 SYMBOLS = [
     "create", "destroy", "last_error", "build_info", "set_problem", "set_ph_terms",
-    "solve", "objective", "xbar", "update_w", "expect", "export_slots", "last_solve_timing",
+    "solve", "objective", "xbar", "update_w", "expect", "export_slots", "last_solve_stats", "jit_info",
 ]
 
 
@@ -101,8 +111,8 @@ class Lib:
                             c_int32, P_i32, P_i32, c_void_p, c_void_p])
         self.expect = fn("expect", ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p])
         self.export_slots = fn("export_slots", ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p])
-        self.last_solve_timing = fn("last_solve_timing", ctypes.c_int,
-                                    [c_void_p, P_f64, P_i32, P_f64, P_f64, P_f64])
+        self.last_solve_stats = fn("last_solve_stats", ctypes.c_int, [c_void_p, ctypes.POINTER(SolveStats)])
+        self.jit_info = fn("jit_info", ctypes.c_char_p, [c_void_p])
 
     def check(self, ctx, rc, what):
         if rc != 0:

@@ -1,0 +1,193 @@
+// phx_jit.h — structure of a small subproblem and the source of its
+// specialised lane-solver kernel (host side; compiled by hipRTC in
+// phx_kernels.hip, instantiated with a runtime pattern by tests/emu).
+//
+// The kernels are specialised on the STRUCTURE (sparsity pattern, column
+// pairs of A D A', nonant column map, which bounds / row sides are finite,
+// which columns are fixed, which rows are equalities) and on the numbers that
+// are the same for every scenario of the batch (scaled constant A entries,
+// costs, bounds, scaling), baked in as exact hex-float literals.  Scenario-
+// varying numbers (varying A entries, PH terms, varying costs/bounds/rhs) stay
+// run-time inputs.  Compiled once per phx_set_problem (cached by source text).
+#pragma once
+#include <stdint.h>
+#include <math.h>
+#include <stdio.h>
+#include <algorithm>
+#include <sstream>
+#include <string>
+#include <vector>
+#include "phx_setup.h"
+
+namespace phx {
+
+struct LaneStructure {
+    int n = 0, m = 0, nnz = 0, npairs = 0, nvar = 0, nslot = 0;
+    bool c_vary = false, bnd_vary = false, rhs_vary = false;
+    std::vector<int32_t> row, col, kvar, col_slot;
+    std::vector<int32_t> pair_a, pair_b, pair_pos;
+    std::vector<uint8_t> lfin, ufin, fixed, blfin, bufin, eq;
+    // scaled scenario-invariant numbers, baked into the kernel as literals
+    // (c / lb,ub / bl,bu only when they do not vary across scenarios)
+    std::vector<double> Ac, dc, dr, c, lb, ub, bl, bu;
+};
+
+// Attach the scaled invariant numbers (host copies of the device arrays).
+inline void set_lane_values(LaneStructure& L, const std::vector<double>& Ac, const std::vector<double>& dc,
+                            const std::vector<double>& dr, const std::vector<double>& c,
+                            const std::vector<double>& lb, const std::vector<double>& ub,
+                            const std::vector<double>& bl, const std::vector<double>& bu) {
+    L.Ac = Ac; L.dc = dc; L.dr = dr;
+    L.c = L.c_vary ? std::vector<double>() : c;
+    L.lb = L.bnd_vary ? std::vector<double>() : lb;
+    L.ub = L.bnd_vary ? std::vector<double>() : ub;
+    L.bl = L.rhs_vary ? std::vector<double>() : bl;
+    L.bu = L.rhs_vary ? std::vector<double>() : bu;
+}
+
+// Limits for the register-resident kernel (beyond them: generic kernels).
+constexpr int LANE_MAX_N = 64;
+constexpr int LANE_MAX_M = 24;
+constexpr int LANE_MAX_NNZ = 384;
+
+// lb/ub/bl/bu: scenario-major host copies of the UNSCALED bounds of every
+// scenario (S rows; S = 1 if invariant).  Returns false (with reason) if the
+// structure is not uniform across scenarios or too large.
+inline bool build_lane_structure(const HostSetup& hs, int n, int m, int nnz, bool c_vary, bool bnd_vary,
+                                 bool rhs_vary, const std::vector<double>& lb, const std::vector<double>& ub,
+                                 const std::vector<double>& bl, const std::vector<double>& bu, int Sb, int Sr,
+                                 LaneStructure& L, std::string& why) {
+    if (n > LANE_MAX_N || m > LANE_MAX_M || nnz > LANE_MAX_NNZ || m < 1 || nnz < 1) {
+        why = "size";
+        return false;
+    }
+    L.n = n; L.m = m; L.nnz = nnz;
+    L.c_vary = c_vary; L.bnd_vary = bnd_vary; L.rhs_vary = rhs_vary;
+    L.row.assign(hs.rowof.begin(), hs.rowof.end());
+    L.col.assign(hs.colidx.begin(), hs.colidx.end());
+    L.kvar.assign(hs.kvar.begin(), hs.kvar.end());
+    L.col_slot.assign(hs.col_slot.begin(), hs.col_slot.end());
+    L.nvar = 0;
+    for (int k = 0; k < nnz; ++k) L.nvar = std::max(L.nvar, hs.kvar[k] + 1);
+    L.nslot = (int)hs.slot_col.size();
+    L.pair_a.clear(); L.pair_b.clear(); L.pair_pos.clear();
+    for (int j = 0; j < n; ++j)
+        for (int a = hs.colptr[j]; a < hs.colptr[j + 1]; ++a)
+            for (int b = hs.colptr[j]; b <= a; ++b) {
+                const int ka = hs.csc2csr[a], kb = hs.csc2csr[b];
+                const int ia = hs.rowof[ka], ib = hs.rowof[kb];
+                const int hi = ia > ib ? ia : ib, lo = ia > ib ? ib : ia;
+                L.pair_a.push_back(ka);
+                L.pair_b.push_back(kb);
+                L.pair_pos.push_back(hi * (hi + 1) / 2 + lo);
+            }
+    L.npairs = (int)L.pair_a.size();
+    auto uni = [&](const std::vector<double>& a, int S, int len, int j, auto pred) -> int {
+        const int v = pred(a[j]) ? 1 : 0;
+        for (int s = 1; s < S; ++s)
+            if ((pred(a[(size_t)s * len + j]) ? 1 : 0) != v) return -1;
+        return v;
+    };
+    L.lfin.assign(n, 0); L.ufin.assign(n, 0); L.fixed.assign(n, 0);
+    for (int j = 0; j < n; ++j) {
+        const int lf = uni(lb, Sb, n, j, [](double v) { return std::isfinite(v); });
+        const int uf = uni(ub, Sb, n, j, [](double v) { return std::isfinite(v); });
+        if (lf < 0 || uf < 0) { why = "bound finiteness varies across scenarios"; return false; }
+        L.lfin[j] = (uint8_t)lf; L.ufin[j] = (uint8_t)uf;
+        int fx = lb[j] == ub[j];
+        for (int s = 1; s < Sb; ++s)
+            if ((lb[(size_t)s * n + j] == ub[(size_t)s * n + j]) != (bool)fx) { why = "fixing varies"; return false; }
+        L.fixed[j] = (uint8_t)fx;
+    }
+    L.blfin.assign(m, 0); L.bufin.assign(m, 0); L.eq.assign(m, 0);
+    for (int i = 0; i < m; ++i) {
+        const int lf = uni(bl, Sr, m, i, [](double v) { return std::isfinite(v); });
+        const int uf = uni(bu, Sr, m, i, [](double v) { return std::isfinite(v); });
+        if (lf < 0 || uf < 0) { why = "row finiteness varies across scenarios"; return false; }
+        L.blfin[i] = (uint8_t)lf; L.bufin[i] = (uint8_t)uf;
+        int e = bl[i] == bu[i];
+        for (int s = 1; s < Sr; ++s)
+            if ((bl[(size_t)s * m + i] == bu[(size_t)s * m + i]) != (bool)e) { why = "equality varies"; return false; }
+        L.eq[i] = (uint8_t)e;
+    }
+    return true;
+}
+
+template <class T>
+inline void emit_table(std::ostringstream& o, const char* ret, const char* name, const std::vector<T>& v) {
+    o << "  __host__ __device__ static constexpr " << ret << " " << name << "(int k) { constexpr " << ret
+      << " a[] = {";
+    for (size_t i = 0; i < v.size(); ++i) o << (i ? "," : "") << (long long)v[i];
+    if (v.empty()) o << "0";
+    o << "}; return a[k]; }\n";
+}
+
+// exact hex-float literal table (non-finite entries are never read: emitted as 0)
+inline void emit_dtable(std::ostringstream& o, const char* name, const std::vector<double>& v) {
+    o << "  __host__ __device__ static constexpr double " << name << "(int k) { constexpr double a[] = {";
+    char buf[64];
+    for (size_t i = 0; i < v.size(); ++i) {
+        snprintf(buf, sizeof(buf), "%a", std::isfinite(v[i]) ? v[i] : 0.0);
+        o << (i ? "," : "") << buf;
+    }
+    if (v.empty()) o << "0.0";
+    o << "}; return a[k]; }\n";
+}
+
+// HIP source of the specialised kernels `phx_lane_ipm` / `phx_lane_polish`
+// (hipRTC input).
+inline std::string lane_kernel_source(const LaneStructure& L) {
+    std::ostringstream o;
+    o << "#include \"phx_lane.h\"\n";
+    o << "struct PT {\n";
+    o << "  static constexpr int NMAX_N = " << L.n << ", NMAX_M = " << L.m << ", NMAX_K = " << L.nnz
+      << ", NMAX_V = " << std::max(L.nvar, 1) << ", NMAX_S = " << std::max(L.nslot, 1) << ";\n";
+    o << "  __host__ __device__ static constexpr int nvar() { return " << L.nvar << "; }\n";
+    o << "  __host__ __device__ static constexpr int nslot() { return " << L.nslot << "; }\n";
+    o << "  __host__ __device__ static constexpr int n() { return " << L.n << "; }\n";
+    o << "  __host__ __device__ static constexpr int m() { return " << L.m << "; }\n";
+    o << "  __host__ __device__ static constexpr int nnz() { return " << L.nnz << "; }\n";
+    o << "  __host__ __device__ static constexpr int npairs() { return " << L.npairs << "; }\n";
+    o << "  __host__ __device__ static constexpr bool c_vary() { return " << (L.c_vary ? "true" : "false") << "; }\n";
+    o << "  __host__ __device__ static constexpr bool bnd_vary() { return " << (L.bnd_vary ? "true" : "false")
+      << "; }\n";
+    o << "  __host__ __device__ static constexpr bool rhs_vary() { return " << (L.rhs_vary ? "true" : "false")
+      << "; }\n";
+    emit_table(o, "int", "row", L.row);
+    emit_table(o, "int", "col", L.col);
+    emit_table(o, "int", "kvar", L.kvar);
+    emit_table(o, "int", "col_slot", L.col_slot);
+    emit_table(o, "int", "pair_a", L.pair_a);
+    emit_table(o, "int", "pair_b", L.pair_b);
+    emit_table(o, "int", "pair_pos", L.pair_pos);
+    emit_table(o, "bool", "lfin", L.lfin);
+    emit_table(o, "bool", "ufin", L.ufin);
+    emit_table(o, "bool", "fixed", L.fixed);
+    emit_table(o, "bool", "blfin", L.blfin);
+    emit_table(o, "bool", "bufin", L.bufin);
+    emit_table(o, "bool", "eq", L.eq);
+    emit_dtable(o, "Ac", L.Ac);
+    emit_dtable(o, "dcs", L.dc);
+    emit_dtable(o, "drs", L.dr);
+    emit_dtable(o, "cs", L.c);
+    emit_dtable(o, "lbs", L.lb);
+    emit_dtable(o, "ubs", L.ub);
+    emit_dtable(o, "bls", L.bl);
+    emit_dtable(o, "bus", L.bu);
+    o << "};\n";
+    o << "extern \"C\" __global__ void __launch_bounds__(64) phx_lane_ipm(phx_lane::LaneIO io, "
+         "const int* lanes, const int* count) {\n"
+         "  const int t = blockIdx.x * 64 + threadIdx.x;\n"
+         "  if (t >= *count) return;\n"
+         "  phx_lane::ipm_lane<PT>(io, lanes ? lanes[t] : t);\n"
+         "}\n";
+    o << "extern \"C\" __global__ void __launch_bounds__(64) phx_lane_polish(phx_lane::LaneIO io, "
+         "const int* lanes, const int* count) {\n"
+         "  const int t = blockIdx.x * 64 + threadIdx.x;\n"
+         "  if (t >= *count) return;\n"
+         "  phx_lane::polish_lane<PT>(io, lanes ? lanes[t] : t);\n"
+         "}\n";
+    return o.str();
+}
+
+}  // namespace phx

@@ -13,7 +13,7 @@ passes solver options (``iter0_solver_options`` / ``iterk_solver_options``,
 phbase.py:273-275): keys ``pdhg_max_iters``, ``pdhg_check_every``,
 ``pdhg_restart_max``, ``polish``, ``polish_refine``, ``polish_below``,
 ``kkt_tol``, ``opt_tol``, ``polish_reg``, ``warm_start``, ``ipm_after``,
-``ipm_max_it``, ``ipm_tol``.
+``ipm_max_it``, ``ipm_tol``, ``lane_solver``.
 """
 import ctypes
 import inspect
@@ -39,6 +39,7 @@ SOLVER_DEFAULTS = {
     "ipm_after": 1024,
     "ipm_max_it": 60,
     "ipm_tol": 1e-10,
+    "lane_solver": 1,
 }
 
 OPTIMAL, ITER_LIMIT, NUMERIC_FAIL = 1, 2, 3
@@ -94,6 +95,7 @@ class SPOpt(SPBase):
         so.ipm_after = int(o["ipm_after"])
         so.ipm_max_it = int(o["ipm_max_it"])
         so.ipm_tol = float(o["ipm_tol"])
+        so.lane_solver = int(o["lane_solver"])
         return so
 
     def _set_ph_terms(self):
@@ -126,18 +128,13 @@ class SPOpt(SPBase):
         self._outer.copy_(self._obj)
         self._conv_cache = None
         self._bump()
-        ms = ctypes.c_double(0)
-        pms = ctypes.c_double(0)
-        la = ctypes.c_int32(0)
-        li = ctypes.c_double(0)
-        ims = ctypes.c_double(0)
-        lib.check(self._ctx, lib.last_solve_timing(self._ctx, ctypes.byref(ms), ctypes.byref(la),
-                                                   ctypes.byref(li), ctypes.byref(pms), ctypes.byref(ims)),
-                  "last_solve_timing")
+        stt = _native.SolveStats()
+        lib.check(self._ctx, lib.last_solve_stats(self._ctx, ctypes.byref(stt)), "last_solve_stats")
         st = self._status
         n_bad = int((st != OPTIMAL).sum().item())
-        self.solve_stats.append({"pdhg_iters": int(total.value), "pdhg_ms": ms.value, "launches": la.value,
-                                 "lane_iters": li.value, "polish_ms": pms.value, "ipm_ms": ims.value,
+        self.solve_stats.append({"pdhg_iters": int(total.value), "pdhg_ms": stt.pdhg_ms, "launches": stt.pdhg_launches,
+                                 "lane_iters": stt.lane_iters, "polish_ms": stt.polish_ms, "ipm_ms": stt.ipm_ms,
+                                 "lane_ms": stt.lane_ms, "lane_polish_ms": stt.lane_polish_ms, "lane_certified": stt.lane_certified,
                                  "wall_s": time.perf_counter() - t0, "not_optimal": n_bad})
         if n_bad and gripe:
             stc = st.cpu().numpy()
