@@ -172,8 +172,9 @@ def main():
         "kernel_ms_per_step": {"pdhg": pdhg_ms / args.steps, "polish": sum(s["polish_ms"] for s in stats) / args.steps,
                                "ipm": sum(s["ipm_ms"] for s in stats) / args.steps,
                                "lane_ipm": sum(s.get("lane_ms", 0.0) for s in stats) / args.steps,
-                               "lane_polish": sum(s.get("lane_polish_ms", 0.0) for s in stats) / args.steps},
+                               "lane_warm": sum(s.get("lane_warm_ms", 0.0) for s in stats) / args.steps},
         "lane_certified_per_step": [s.get("lane_certified") for s in stats],
+        "lane_warm_certified_per_step": [s.get("lane_warm_certified") for s in stats],
         "solver_options": solver_opts,
         "not_optimal": sum(s["not_optimal"] for s in stats),
         "setup_s": t_setup, "iter0_s": t_iter0,

@@ -81,6 +81,9 @@ typedef struct phx_solve_opts {
     int32_t lane_solver;      /* 1: run the register-resident, structure-
                                  specialised lane solver (IPM + polish) first
                                  when the context has one (small subproblems) */
+    int32_t as_rounds;        /* active-set rounds per lane-solver kernel; 0
+                                 disables the warm active-set pass (each solve
+                                 then starts with the interior point)        */
 } phx_solve_opts;
 
 /* Statistics of the most recent phx_solve (HIP events on the solve stream). */
@@ -88,12 +91,14 @@ typedef struct phx_solve_stats {
     double  pdhg_ms;          /* summed k_chunk (PDHG) kernel time            */
     double  polish_ms;        /* summed k_polish time                         */
     double  ipm_ms;           /* generic interior-point finisher              */
-    double  lane_ms;          /* specialised lane IPM kernel                  */
-    double  lane_polish_ms;   /* specialised lane polish kernel               */
+    double  lane_ms;          /* specialised lane kernel: IPM + active set    */
+    double  lane_warm_ms;     /* specialised lane kernel: warm active set     */
     double  lane_iters;       /* PDHG scenario-iterations executed            */
     int32_t pdhg_launches;
     int32_t total_iters;      /* PDHG iterations of the batch loop            */
     int32_t lane_certified;   /* scenarios certified by the lane solver       */
+    int32_t lane_warm_certified; /* ... of which by the warm active-set pass  */
+    int32_t not_optimal;      /* scenarios without an optimal status          */
     int32_t jit;              /* 1 if this context has a specialised kernel   */
 } phx_solve_stats;
 
@@ -115,6 +120,8 @@ typedef struct phx_tree_desc {
     const int32_t* node_nlen;  /* [nnodes]                                    */
     int32_t NNS;               /* global number of (node, slot) entries       */
     int32_t npart;             /* size of the partial buffer (doubles)        */
+    int32_t nnodes_cover;      /* sum of node_nlen over the local nodes (== NNS
+                                  when every node has a local scenario)       */
 } phx_tree_desc;
 
 /* ---- lifetime ---------------------------------------------------------- */
@@ -170,9 +177,12 @@ int phx_xbar(phx_ctx* ctx, const phx_tree_desc* tree, const double* x,
 
 /* Update_W + convergence_diff local part (phbase.py:293-343):
  *   W[j][s] += rho[j][s]*(x_N - xbar)   (if update_w)
- *   dsum[s]  = sum_j |x_N - xbar|
+ *   dsum[s]  = sum_j |x_N - xbar|            (dsum may be NULL when the
+ *                                             segments cover every scenario)
  * then seg_sums[r] = sum of dsum over local scenarios [seg_s0[r], seg_s1[r])
- * (one segment per emulated reference rank, sputils.py:803-810).           */
+ * (one segment per emulated reference rank, sputils.py:803-810).  When the
+ * segments partition the local scenarios, W, dsum and the segment partials
+ * come out of one fused pass (k_update_w_seg).                              */
 int phx_update_w(phx_ctx* ctx, const double* x, const double* xbar_node,
                  const int32_t* xbar_idx, const double* rho, double* W,
                  int32_t update_w, double* dsum, int32_t nseg,

@@ -136,7 +136,7 @@ inline void emit_dtable(std::ostringstream& o, const char* name, const std::vect
 
 // HIP source of the specialised kernels `phx_lane_ipm` / `phx_lane_polish`
 // (hipRTC input).
-inline std::string lane_kernel_source(const LaneStructure& L) {
+inline std::string lane_kernel_source(const LaneStructure& L, int warm_waves = 1) {
     std::ostringstream o;
     o << "#include \"phx_lane.h\"\n";
     o << "struct PT {\n";
@@ -169,23 +169,34 @@ inline std::string lane_kernel_source(const LaneStructure& L) {
     emit_dtable(o, "Ac", L.Ac);
     emit_dtable(o, "dcs", L.dc);
     emit_dtable(o, "drs", L.dr);
+    {
+        std::vector<double> idc(L.dc.size()), idr(L.dr.size());
+        for (size_t j = 0; j < idc.size(); ++j) idc[j] = 1.0 / L.dc[j];
+        for (size_t i = 0; i < idr.size(); ++i) idr[i] = 1.0 / L.dr[i];
+        emit_dtable(o, "idcs", idc);
+        emit_dtable(o, "idrs", idr);
+    }
     emit_dtable(o, "cs", L.c);
     emit_dtable(o, "lbs", L.lb);
     emit_dtable(o, "ubs", L.ub);
     emit_dtable(o, "bls", L.bl);
     emit_dtable(o, "bus", L.bu);
     o << "};\n";
-    o << "extern \"C\" __global__ void __launch_bounds__(64) phx_lane_ipm(phx_lane::LaneIO io, "
-         "const int* lanes, const int* count) {\n"
+    o << "extern \"C\" __global__ void __launch_bounds__(64, " << warm_waves
+      << ") phx_lane_warm(phx_lane::LaneIO io) {\n"
          "  const int t = blockIdx.x * 64 + threadIdx.x;\n"
-         "  if (t >= *count) return;\n"
-         "  phx_lane::ipm_lane<PT>(io, lanes ? lanes[t] : t);\n"
+         "  bool still = false;\n"
+         "  if (t < io.S) still = phx_lane::warm_lane<PT>(io, t);\n"
+         "  phx_lane::compact_lane(still, t, io.lanes_out, io.count_out);\n"
          "}\n";
-    o << "extern \"C\" __global__ void __launch_bounds__(64) phx_lane_polish(phx_lane::LaneIO io, "
+    o << "extern \"C\" __global__ void __launch_bounds__(64) phx_lane_cold(phx_lane::LaneIO io, "
          "const int* lanes, const int* count) {\n"
          "  const int t = blockIdx.x * 64 + threadIdx.x;\n"
-         "  if (t >= *count) return;\n"
-         "  phx_lane::polish_lane<PT>(io, lanes ? lanes[t] : t);\n"
+         "  const int nl = count ? *count : io.S;\n"
+         "  bool still = false;\n"
+         "  int sc = -1;\n"
+         "  if (t < nl) { sc = lanes ? lanes[t] : t; still = phx_lane::cold_lane<PT>(io, sc); }\n"
+         "  phx_lane::compact_lane(still, sc, io.lanes_out, io.count_out);\n"
          "}\n";
     return o.str();
 }

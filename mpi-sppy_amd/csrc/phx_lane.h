@@ -9,22 +9,28 @@
 // infinite bounds and their updates vanish) and keeps the per-lane vectors in
 // VGPRs.  Scenario-invariant numbers (constant A entries, costs, bounds,
 // scaling) are baked in as exact literals (one kernel per problem, compiled at
-// phx_set_problem); only scenario-varying values occupy vector registers.  The same templates compile on the host with a runtime pattern
-// (tests/emu), which is how the CPU suite checks them.
+// phx_set_problem); only scenario-varying values occupy vector registers.  The
+// same templates compile on the host with a runtime pattern (tests/emu), which
+// is how the CPU suite checks them.
 //
 // Two kernels per solve (phx_jit.h emits both):
-//   phx_lane_ipm     Mehrotra predictor-corrector IPM on
+//   phx_lane_warm   active-set solve seeded with the lane's active set of the
+//                   previous solve (PH subproblems change little from one PH
+//                   iteration to the next): equality-constrained KKT solve ->
+//                   certificate -> primal-dual active-set update, a few rounds.
+//   phx_lane_cold   Mehrotra predictor-corrector IPM on
 //                      min 0.5 x'Px + q'x  s.t. Ax - s = 0, l <= x <= u,
 //                      bl <= s <= bu
-//                    normal matrix M = A (P+Sx)^-1 A' + Ss^-1 (packed
-//                    Cholesky).  Bound-multiplier steps are recomputed from
-//                    (dx, ds) instead of stored.  Writes (x, y) to xT/yT and
-//                    the PDHG warm start (phx_core.h conventions).
-//   phx_lane_polish  active-set KKT polish from (xT, yT): classification by
-//                    slack-vs-multiplier (sharp at IPM points), quasi-definite
-//                    regularised KKT + iterative refinement, KKT certificate.
-// Lanes that fail the certificate continue on the generic PDHG path from the
-// IPM point.
+//                   (normal matrix M = A (P+Sx)^-1 A' + Ss^-1, packed Cholesky
+//                   with dependent-pivot replacement), then the active set read
+//                   off the IPM point (slack vs multiplier, sharp by strict
+//                   complementarity) and the same KKT/certificate/active-set
+//                   rounds.  Runs on the lanes the warm kernel did not certify
+//                   (all lanes on a first solve).
+// A certified lane writes its unscaled solution, row duals and objective
+// straight to the caller's outputs and stores its active set for the next
+// solve.  Lanes that fail the certificate continue on the generic PDHG path
+// (phx_core.h) from the IPM point.
 #pragma once
 #if !defined(__HIPCC_RTC__)
 #include <stdint.h>
@@ -35,6 +41,8 @@
 #else
 typedef long long int64_t;   // hipRTC: no libc headers; hip_runtime provides the math
 typedef int int32_t;
+typedef unsigned int uint32_t;
+typedef unsigned long long uint64_t;
 #endif
 
 #if defined(__HIPCC__) || defined(__HIPCC_RTC__)
@@ -45,40 +53,70 @@ typedef int int32_t;
 #define PHX_UNROLL
 #endif
 
+// Diagnostics hook (the CPU emulation defines it to record why a lane failed;
+// a no-op in the GPU kernels).
+#ifndef PHX_LANE_FAIL
+#define PHX_LANE_FAIL(code, idx)
+#endif
+#ifndef PHX_LANE_STAT
+#define PHX_LANE_STAT(kind)
+#endif
+
 namespace phx_lane {
 
 PHX_LD int tri(int i, int k) { return i * (i + 1) / 2 + k; }   // i >= k
 PHX_LD double clampd(double v, double lo, double hi) { return fmin(fmax(v, lo), hi); }
 
+// active-set words: 2 bits per column (0 free, 1 at lower, 2 at upper) then
+// 2 bits per row (0 inactive, 1 lower side active, 2 upper side active)
+PHX_LD constexpr int aset_words(int n, int m) { return (2 * (n + m) + 31) / 32; }
+
+// Active-set KKT solves: quasi-definite regularisation and the cap on its
+// iterative-refinement steps (compile-time, so the refinement is unrolled and
+// 1/(p+reg) of the LP columns folds to a constant).
+constexpr double KKT_REG = 1e-6;
+constexpr int KKT_REFINE = 6;
+
+// flags bits shared with the host / generic path
+constexpr int32_t FLAG_IPM_TRIED = 1;   // interior point already attempted
+constexpr int32_t FLAG_WRITTEN = 2;     // outputs written by a lane kernel
+
 // Runtime inputs/outputs (device pointers; per-scenario arrays [i*S + s]).
 struct LaneIO {
     int32_t S;
-    const double* Ac;      // scaled invariant A values [nnz]
-    const double* dr;      // row scaling [m]
-    const double* dc;      // column scaling [n]
     const double* Av;      // varying scaled A values [nvar*S]
-    const double* c;       // scaled c   [n] or [n*S] (PT::c_vary())
-    const double* lb;      // scaled lb  [n] or [n*S] (PT::bnd_vary())
+    const double* c;       // scaled c   [n*S] (only read if PT::c_vary())
+    const double* lb;      // scaled lb  [n*S] (PT::bnd_vary())
     const double* ub;
-    const double* bl;      // scaled bl  [m] or [m*S] (PT::rhs_vary())
+    const double* bl;      // scaled bl  [m*S] (PT::rhs_vary())
     const double* bu;
     const double* qN;      // unscaled PH linear term [N*S]
     const double* pN;      // unscaled PH quadratic   [N*S]
-    double* xT;            // scaled x [n*S]
+    const double* kN;      // unscaled PH constant    [S]
+    double* xT;            // scaled x [n*S]   (generic-path hand-over)
     double* yT;            // scaled y [m*S]
     double* x;             // PDHG warm start (= xT)
     double* y;
     double* x0;
     double* y0;
     double* err;           // [S]
-    int32_t* status;       // [S]: 1 certified, 0 hand over to PDHG
+    int32_t* status;       // [S]: 1 certified, 0 running (generic path)
     int32_t* iters;        // [S]: IPM iterations used
-    int32_t* flags;        // [S]: bit0 set (IPM attempted)
+    int32_t* flags;        // [S]: FLAG_* bits
+    uint32_t* aset;        // [aset_words(n,m)*S] active set of the last certified solve
+    double* x_out;         // unscaled x [n*S]
+    double* y_out;         // unscaled row duals [m*S] (may be null)
+    double* obj_out;       // [S] objective incl. PH terms
+    int32_t* status_out;   // [S] caller's status (1 optimal)
+    int32_t* iters_out;    // [S] caller's iteration counts
+    int32_t* lanes_out;    // compacted uncertified lanes
+    int32_t* count_out;    // their number (atomic)
     int32_t max_it;
     double ipm_tol;
     double kkt_tol;
     double reg;
     int32_t refine;
+    int32_t as_rounds;     // active-set rounds per kernel
 };
 
 // Data access for one lane: scenario-varying numbers in registers; the
@@ -102,9 +140,11 @@ struct Data {
     PHX_LD double A(int k) const { return PT::kvar(k) < 0 ? PT::Ac(k) : av[PT::kvar(k)]; }
     PHX_LD double dc(int j) const { return PT::dcs(j); }
     PHX_LD double dr(int i) const { return PT::drs(i); }
+    PHX_LD double idc(int j) const { return PT::idcs(j); }   // 1/dc
+    PHX_LD double idr(int i) const { return PT::idrs(i); }   // 1/dr
+    PHX_LD double c(int j) const { return PT::c_vary() ? io.c[(int64_t)j * io.S + sc] : PT::cs(j); }
     PHX_LD double q(int j) const {
-        const double c = PT::c_vary() ? io.c[(int64_t)j * io.S + sc] : PT::cs(j);
-        return PT::col_slot(j) >= 0 ? c + dc(j) * qn[PT::col_slot(j)] : c;
+        return PT::col_slot(j) >= 0 ? c(j) + dc(j) * qn[PT::col_slot(j)] : c(j);
     }
     PHX_LD double p(int j) const {
         return PT::col_slot(j) >= 0 ? dc(j) * dc(j) * pn[PT::col_slot(j)] : 0.0;
@@ -164,18 +204,25 @@ struct Data {
     }
 };
 
-// packed Cholesky (lower, in place); false if not positive definite
+// Packed Cholesky (lower, in place).  A pivot that collapses relative to its
+// original diagonal (a dependent row of A D A' near an interior-point
+// optimum) is replaced by a huge value, which zeroes that component of the
+// solve — the classic IPM safeguard.  Returns false only on a non-finite or
+// non-positive original diagonal.
 template <class PT>
-PHX_LD bool cholesky(double* M) {
+PHX_LD bool cholesky_ipm(double* M, double* idg) {
     bool ok = true;
     PHX_UNROLL for (int jj = 0; jj < PT::m(); ++jj) {
-        double d = M[tri(jj, jj)];
+        const double d0 = M[tri(jj, jj)];
+        double d = d0;
         PHX_UNROLL for (int k = 0; k < PT::m(); ++k)
             if (k < jj) d -= M[tri(jj, k)] * M[tri(jj, k)];
-        ok = ok && (d > 0.0);
-        d = sqrt(fmax(d, 1e-300));
+        ok = ok && (d0 > 0.0) && (d0 < 1e300);
+        if (!(d > 1e-13 * d0)) d = 1e128;
+        d = sqrt(d);
         M[tri(jj, jj)] = d;
         const double inv = 1.0 / d;
+        idg[jj] = inv;
         PHX_UNROLL for (int i = 0; i < PT::m(); ++i) {
             if (i > jj) {
                 double v = M[tri(i, jj)];
@@ -188,32 +235,49 @@ PHX_LD bool cholesky(double* M) {
     return ok;
 }
 
-// solve (L L') t = t ; diagonal stored as its reciprocal is not assumed
+// Plain packed Cholesky; false if not (numerically) positive definite.
+// idg[i] receives 1/L_ii for the multiplication-only solve.
 template <class PT>
-PHX_LD void chol_solve(const double* M, double* t) {
+PHX_LD bool cholesky(double* M, double* idg) {
+    bool ok = true;
+    PHX_UNROLL for (int jj = 0; jj < PT::m(); ++jj) {
+        double d = M[tri(jj, jj)];
+        PHX_UNROLL for (int k = 0; k < PT::m(); ++k)
+            if (k < jj) d -= M[tri(jj, k)] * M[tri(jj, k)];
+        ok = ok && (d > 0.0);
+        d = sqrt(fmax(d, 1e-300));
+        M[tri(jj, jj)] = d;
+        const double inv = 1.0 / d;
+        idg[jj] = inv;
+        PHX_UNROLL for (int i = 0; i < PT::m(); ++i) {
+            if (i > jj) {
+                double v = M[tri(i, jj)];
+                PHX_UNROLL for (int k = 0; k < PT::m(); ++k)
+                    if (k < jj) v -= M[tri(i, k)] * M[tri(jj, k)];
+                M[tri(i, jj)] = v * inv;
+            }
+        }
+    }
+    return ok;
+}
+
+// solve (L L') t = t with the reciprocal diagonal idg
+template <class PT>
+PHX_LD void chol_solve_inv(const double* M, const double* idg, double* t) {
     PHX_UNROLL for (int i = 0; i < PT::m(); ++i) {
         double v = t[i];
         PHX_UNROLL for (int k = 0; k < PT::m(); ++k)
             if (k < i) v -= M[tri(i, k)] * t[k];
-        t[i] = v / M[tri(i, i)];
+        t[i] = v * idg[i];
     }
     PHX_UNROLL for (int ii = 0; ii < PT::m(); ++ii) {
         const int i = PT::m() - 1 - ii;
         double v = t[i];
         PHX_UNROLL for (int k = 0; k < PT::m(); ++k)
             if (k > i) v -= M[tri(k, i)] * t[k];
-        t[i] = v / M[tri(i, i)];
+        t[i] = v * idg[i];
     }
 }
-
-// Complementarity right-hand sides with Mehrotra's second-order term.
-// Lower side (slack sl = x - l, multiplier z, affine step da):
-//   dz_aff = -z (sl + da) / sl,  c = smu - sl z - da dz_aff,  dz = (c - z dx) / sl
-// Upper side (slack sl = u - x):
-//   dz_aff =  z (da - sl) / sl,  c = smu - sl z + da dz_aff,  dz = (c + z dx) / sl
-// (da = 0 in the predictor pass gives the plain affine system.)
-PHX_LD double comp_lo(double sl, double z, double smu, double da) { return smu - sl * z + da * z * (sl + da) / sl; }
-PHX_LD double comp_up(double sl, double z, double smu, double da) { return smu - sl * z + da * z * (da - sl) / sl; }
 
 template <class PT>
 PHX_LD bool has_lo(int j) { return PT::lfin(j) && !PT::fixed(j); }
@@ -227,15 +291,27 @@ template <class PT>
 PHX_LD bool row_free(int i) { return !PT::blfin(i) && !PT::bufin(i); }
 
 // ---------------------------------------------------------------------------
-// IPM kernel body
+// Interior point (Mehrotra predictor-corrector).  Complementarity right-hand
+// sides with the second-order term, written with the reciprocal slack r = 1/sl
+// (one division per bound per iteration):
+//   lower:  comp = smu - sl z + da z (sl + da) r,   dz = (comp - z dx) r
+//   upper:  comp = smu - sl z + da z (da - sl) r,   dz = (comp + z dx) r
+// (da = affine step of the slack's variable, 0 in the predictor pass).
+// Returns the relative KKT error of (x, y); *its = iterations used.
 // ---------------------------------------------------------------------------
+PHX_LD double comp_lo(double sl, double r, double z, double smu, double da) {
+    return smu - sl * z + da * z * (sl + da) * r;
+}
+PHX_LD double comp_up(double sl, double r, double z, double smu, double da) {
+    return smu - sl * z + da * z * (da - sl) * r;
+}
+
 template <class PT>
-PHX_LD void ipm_lane(const LaneIO& io, int sc) {
+PHX_LD double ipm_core(const Data<PT>& D, int max_it, double tol, double* x, double* y, int* its) {
     constexpr int NN = PT::NMAX_N, MM = PT::NMAX_M, TT = PT::NMAX_M * (PT::NMAX_M + 1) / 2;
-    const Data<PT> D(io, sc);
     const double reg = 1e-10;
-    double x[NN], zl[NN], zu[NN], s[MM], y[MM], wl[MM], wu[MM];
-    // start point (cost-aware multipliers, phx_core.h ipm_lane)
+    double zl[NN], zu[NN], s[MM], wl[MM], wu[MM];
+    // start point (cost-aware multipliers)
     PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
         double xv = 0.0;
         if (PT::fixed(j)) xv = D.l(j);
@@ -269,43 +345,50 @@ PHX_LD void ipm_lane(const LaneIO& io, int sc) {
     double ncomp = 0.0;
     PHX_UNROLL for (int j = 0; j < PT::n(); ++j) ncomp += (has_lo<PT>(j) ? 1.0 : 0.0) + (has_up<PT>(j) ? 1.0 : 0.0);
     PHX_UNROLL for (int i = 0; i < PT::m(); ++i) ncomp += (row_lo<PT>(i) ? 1.0 : 0.0) + (row_up<PT>(i) ? 1.0 : 0.0);
+    const double inv_ncomp = ncomp > 0.0 ? 1.0 / ncomp : 0.0;
     double err = 1e300;
     int it = 0;
-    for (; it < io.max_it; ++it) {
+    for (; it < max_it; ++it) {
         err = D.kkt(x, y);
-        if (err < io.ipm_tol || !(err < 1e300)) break;
+        if (err < tol || !(err < 1e300)) break;
+        // reciprocal slacks
+        double rl[NN], ru[NN], rwl[MM], rwu[MM];
         double mu = 0.0;
         PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
+            rl[j] = has_lo<PT>(j) ? 1.0 / (x[j] - D.l(j)) : 0.0;
+            ru[j] = has_up<PT>(j) ? 1.0 / (D.u(j) - x[j]) : 0.0;
             if (has_lo<PT>(j)) mu += (x[j] - D.l(j)) * zl[j];
             if (has_up<PT>(j)) mu += (D.u(j) - x[j]) * zu[j];
         }
         PHX_UNROLL for (int i = 0; i < PT::m(); ++i) {
+            rwl[i] = row_lo<PT>(i) ? 1.0 / (s[i] - D.bl(i)) : 0.0;
+            rwu[i] = row_up<PT>(i) ? 1.0 / (D.bu(i) - s[i]) : 0.0;
             if (row_lo<PT>(i)) mu += (s[i] - D.bl(i)) * wl[i];
             if (row_up<PT>(i)) mu += (D.bu(i) - s[i]) * wu[i];
         }
-        mu = ncomp > 0.0 ? mu / ncomp : 0.0;
+        mu *= inv_ncomp;
         // normal matrix
-        double Dx[NN], sig[MM], M[TT];
+        double Dx[NN], isig[MM], M[TT], idg[MM];
         PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
             double h = D.p(j) + reg;
-            if (has_lo<PT>(j)) h += zl[j] / (x[j] - D.l(j));
-            if (has_up<PT>(j)) h += zu[j] / (D.u(j) - x[j]);
+            if (has_lo<PT>(j)) h += zl[j] * rl[j];
+            if (has_up<PT>(j)) h += zu[j] * ru[j];
             Dx[j] = PT::fixed(j) ? 0.0 : 1.0 / h;
         }
         PHX_UNROLL for (int t = 0; t < TT; ++t) M[t] = 0.0;
         PHX_UNROLL for (int i = 0; i < PT::m(); ++i) {
             double sg = 0.0;
-            if (row_lo<PT>(i)) sg += wl[i] / (s[i] - D.bl(i));
-            if (row_up<PT>(i)) sg += wu[i] / (D.bu(i) - s[i]);
-            sig[i] = sg;
-            M[tri(i, i)] = row_free<PT>(i) ? 1.0 : (PT::eq(i) ? reg : 1.0 / sg + reg);
+            if (row_lo<PT>(i)) sg += wl[i] * rwl[i];
+            if (row_up<PT>(i)) sg += wu[i] * rwu[i];
+            isig[i] = (row_lo<PT>(i) || row_up<PT>(i)) ? 1.0 / sg : 0.0;
+            M[tri(i, i)] = row_free<PT>(i) ? 1.0 : (PT::eq(i) ? reg : isig[i] + reg);
         }
         PHX_UNROLL for (int t = 0; t < PT::npairs(); ++t) {
             const int ka = PT::pair_a(t), kb = PT::pair_b(t);
             if (!row_free<PT>(PT::row(ka)) && !row_free<PT>(PT::row(kb)))
                 M[PT::pair_pos(t)] += D.A(ka) * Dx[PT::col(ka)] * D.A(kb);
         }
-        if (!cholesky<PT>(M)) break;
+        if (!cholesky_ipm<PT>(M, idg)) { PHX_LANE_FAIL(20, it); break; }
         // predictor (pass 0, smu = 0) then corrector (pass 1)
         double smu = 0.0, ap = 1.0, ad = 1.0;
         double dx[NN], ds[MM], dy[MM], dxa[NN], dsa[MM];
@@ -320,11 +403,11 @@ PHX_LD void ipm_lane(const LaneIO& io, int sc) {
                     double r = aty[j] - D.p(j) * x[j] - D.q(j);
                     if (has_lo<PT>(j)) {
                         const double sl = x[j] - D.l(j);
-                        r += zl[j] + comp_lo(sl, zl[j], smu, dxa[j]) / sl;
+                        r += zl[j] + comp_lo(sl, rl[j], zl[j], smu, dxa[j]) * rl[j];
                     }
                     if (has_up<PT>(j)) {
                         const double sl = D.u(j) - x[j];
-                        r -= zu[j] + comp_up(sl, zu[j], smu, dxa[j]) / sl;
+                        r -= zu[j] + comp_up(sl, ru[j], zu[j], smu, dxa[j]) * ru[j];
                     }
                     dx[j] = PT::fixed(j) ? 0.0 : r * Dx[j];      // H^-1 rho_x
                 }
@@ -334,19 +417,19 @@ PHX_LD void ipm_lane(const LaneIO& io, int sc) {
                     double rhos = -y[i];
                     if (row_lo<PT>(i)) {
                         const double sl = s[i] - D.bl(i);
-                        rhos += wl[i] + comp_lo(sl, wl[i], smu, dsa[i]) / sl;
+                        rhos += wl[i] + comp_lo(sl, rwl[i], wl[i], smu, dsa[i]) * rwl[i];
                     }
                     if (row_up<PT>(i)) {
                         const double sl = D.bu(i) - s[i];
-                        rhos -= wu[i] + comp_up(sl, wu[i], smu, dsa[i]) / sl;
+                        rhos -= wu[i] + comp_up(sl, rwu[i], wu[i], smu, dsa[i]) * rwu[i];
                     }
                     ds[i] = rhos;
                     if (row_free<PT>(i)) dy[i] = 0.0;
                     else if (PT::eq(i)) dy[i] = -(ax[i] - D.bl(i)) - ahr[i];
-                    else dy[i] = -(ax[i] - s[i]) + rhos / sig[i] - ahr[i];
+                    else dy[i] = -(ax[i] - s[i]) + rhos * isig[i] - ahr[i];
                 }
             }
-            chol_solve<PT>(M, dy);
+            chol_solve_inv<PT>(M, idg, dy);
             {
                 double atdy[NN];
                 D.matvec_t(dy, atdy);
@@ -354,49 +437,51 @@ PHX_LD void ipm_lane(const LaneIO& io, int sc) {
                     if (!PT::fixed(j)) dx[j] += Dx[j] * atdy[j];
             }
             PHX_UNROLL for (int i = 0; i < PT::m(); ++i)
-                ds[i] = (PT::eq(i) || row_free<PT>(i)) ? 0.0 : (ds[i] - dy[i]) / sig[i];
-            // step lengths (multiplier steps recomputed from dx, ds)
-            ap = 1.0;
-            ad = 1.0;
-            double maff = 0.0;
+                ds[i] = (PT::eq(i) || row_free<PT>(i)) ? 0.0 : (ds[i] - dy[i]) * isig[i];
+            // step lengths as inverse ratios (step = 1 / max(1, max ratio)),
+            // multiplier steps recomputed from dx, ds
+            double apr = 1.0, adr = 1.0;
             PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
                 if (has_lo<PT>(j)) {
                     const double sl = x[j] - D.l(j);
-                    const double dz = (comp_lo(sl, zl[j], smu, dxa[j]) - zl[j] * dx[j]) / sl;
-                    if (dx[j] < 0.0) ap = fmin(ap, -sl / dx[j]);
-                    if (dz < 0.0) ad = fmin(ad, -zl[j] / dz);
+                    const double dz = (comp_lo(sl, rl[j], zl[j], smu, dxa[j]) - zl[j] * dx[j]) * rl[j];
+                    apr = fmax(apr, -dx[j] * rl[j]);
+                    adr = fmax(adr, -dz / zl[j]);
                 }
                 if (has_up<PT>(j)) {
                     const double sl = D.u(j) - x[j];
-                    const double dz = (comp_up(sl, zu[j], smu, dxa[j]) + zu[j] * dx[j]) / sl;
-                    if (dx[j] > 0.0) ap = fmin(ap, sl / dx[j]);
-                    if (dz < 0.0) ad = fmin(ad, -zu[j] / dz);
+                    const double dz = (comp_up(sl, ru[j], zu[j], smu, dxa[j]) + zu[j] * dx[j]) * ru[j];
+                    apr = fmax(apr, dx[j] * ru[j]);
+                    adr = fmax(adr, -dz / zu[j]);
                 }
             }
             PHX_UNROLL for (int i = 0; i < PT::m(); ++i) {
                 if (row_lo<PT>(i)) {
                     const double sl = s[i] - D.bl(i);
-                    const double dw = (comp_lo(sl, wl[i], smu, dsa[i]) - wl[i] * ds[i]) / sl;
-                    if (ds[i] < 0.0) ap = fmin(ap, -sl / ds[i]);
-                    if (dw < 0.0) ad = fmin(ad, -wl[i] / dw);
+                    const double dw = (comp_lo(sl, rwl[i], wl[i], smu, dsa[i]) - wl[i] * ds[i]) * rwl[i];
+                    apr = fmax(apr, -ds[i] * rwl[i]);
+                    adr = fmax(adr, -dw / wl[i]);
                 }
                 if (row_up<PT>(i)) {
                     const double sl = D.bu(i) - s[i];
-                    const double dw = (comp_up(sl, wu[i], smu, dsa[i]) + wu[i] * ds[i]) / sl;
-                    if (ds[i] > 0.0) ap = fmin(ap, sl / ds[i]);
-                    if (dw < 0.0) ad = fmin(ad, -wu[i] / dw);
+                    const double dw = (comp_up(sl, rwu[i], wu[i], smu, dsa[i]) + wu[i] * ds[i]) * rwu[i];
+                    apr = fmax(apr, ds[i] * rwu[i]);
+                    adr = fmax(adr, -dw / wu[i]);
                 }
             }
+            ap = 1.0 / apr;
+            ad = 1.0 / adr;
             if (pass == 0) {
+                double maff = 0.0;
                 PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
                     if (has_lo<PT>(j)) {
                         const double sl = x[j] - D.l(j);
-                        const double dz = -zl[j] * (sl + dx[j]) / sl;
+                        const double dz = -zl[j] * (sl + dx[j]) * rl[j];
                         maff += (sl + ap * dx[j]) * (zl[j] + ad * dz);
                     }
                     if (has_up<PT>(j)) {
                         const double sl = D.u(j) - x[j];
-                        const double dz = zu[j] * (dx[j] - sl) / sl;
+                        const double dz = zu[j] * (dx[j] - sl) * ru[j];
                         maff += (sl - ap * dx[j]) * (zu[j] + ad * dz);
                     }
                     dxa[j] = dx[j];
@@ -404,17 +489,17 @@ PHX_LD void ipm_lane(const LaneIO& io, int sc) {
                 PHX_UNROLL for (int i = 0; i < PT::m(); ++i) {
                     if (row_lo<PT>(i)) {
                         const double sl = s[i] - D.bl(i);
-                        const double dw = -wl[i] * (sl + ds[i]) / sl;
+                        const double dw = -wl[i] * (sl + ds[i]) * rwl[i];
                         maff += (sl + ap * ds[i]) * (wl[i] + ad * dw);
                     }
                     if (row_up<PT>(i)) {
                         const double sl = D.bu(i) - s[i];
-                        const double dw = wu[i] * (ds[i] - sl) / sl;
+                        const double dw = wu[i] * (ds[i] - sl) * rwu[i];
                         maff += (sl - ap * ds[i]) * (wu[i] + ad * dw);
                     }
                     dsa[i] = ds[i];
                 }
-                maff = ncomp > 0.0 ? maff / ncomp : 0.0;
+                maff *= inv_ncomp;
                 const double ratio = mu > 0.0 ? maff / mu : 0.0;
                 smu = ratio * ratio * ratio * mu;
             }
@@ -425,28 +510,340 @@ PHX_LD void ipm_lane(const LaneIO& io, int sc) {
         PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
             if (has_lo<PT>(j)) {
                 const double sl = x[j] - D.l(j);
-                zl[j] += ad * (comp_lo(sl, zl[j], smu, dxa[j]) - zl[j] * dx[j]) / sl;
+                zl[j] += ad * (comp_lo(sl, rl[j], zl[j], smu, dxa[j]) - zl[j] * dx[j]) * rl[j];
             }
             if (has_up<PT>(j)) {
                 const double sl = D.u(j) - x[j];
-                zu[j] += ad * (comp_up(sl, zu[j], smu, dxa[j]) + zu[j] * dx[j]) / sl;
+                zu[j] += ad * (comp_up(sl, ru[j], zu[j], smu, dxa[j]) + zu[j] * dx[j]) * ru[j];
             }
             x[j] += ap * dx[j];
         }
         PHX_UNROLL for (int i = 0; i < PT::m(); ++i) {
             if (row_lo<PT>(i)) {
                 const double sl = s[i] - D.bl(i);
-                wl[i] += ad * (comp_lo(sl, wl[i], smu, dsa[i]) - wl[i] * ds[i]) / sl;
+                wl[i] += ad * (comp_lo(sl, rwl[i], wl[i], smu, dsa[i]) - wl[i] * ds[i]) * rwl[i];
             }
             if (row_up<PT>(i)) {
                 const double sl = D.bu(i) - s[i];
-                wu[i] += ad * (comp_up(sl, wu[i], smu, dsa[i]) + wu[i] * ds[i]) / sl;
+                wu[i] += ad * (comp_up(sl, rwu[i], wu[i], smu, dsa[i]) + wu[i] * ds[i]) * rwu[i];
             }
             s[i] += ap * ds[i];
             y[i] += ad * dy[i];
         }
     }
+    *its = it;
+    return err;
+}
+
+// ---------------------------------------------------------------------------
+// Active set of one lane.  F[j]: column free; up[j]: a non-free column sits at
+// its upper bound (else lower; fixed columns: lower).  R[i]: row active;
+// lo[i]: at its lower side (equality rows: always active, lower).
+// ---------------------------------------------------------------------------
+// Kept as per-lane bit masks in vector registers (per-lane bool arrays would
+// become 64-bit exec-style lane masks in scalar registers and spill).
+template <class PT>
+struct ASet {
+    uint64_t f = 0, u = 0;   // column j: bit j
+    uint32_t r = 0, l = 0;   // row i: bit i
+    PHX_LD bool F(int j) const { return (f >> j) & 1ull; }
+    PHX_LD bool up(int j) const { return (u >> j) & 1ull; }
+    PHX_LD bool R(int i) const { return (r >> i) & 1u; }
+    PHX_LD bool lo(int i) const { return (l >> i) & 1u; }
+    PHX_LD void setF(int j, bool v) { f = v ? (f | (1ull << j)) : (f & ~(1ull << j)); }
+    PHX_LD void setUp(int j, bool v) { u = v ? (u | (1ull << j)) : (u & ~(1ull << j)); }
+    PHX_LD void setR(int i, bool v) { r = v ? (r | (1u << i)) : (r & ~(1u << i)); }
+    PHX_LD void setLo(int i, bool v) { l = v ? (l | (1u << i)) : (l & ~(1u << i)); }
+};
+
+template <class PT>
+PHX_LD void aset_load(const LaneIO& io, int sc, ASet<PT>& a) {
+    constexpr int NW = aset_words(PT::NMAX_N, PT::NMAX_M);
+    uint32_t w[NW];
+    PHX_UNROLL for (int k = 0; k < aset_words(PT::n(), PT::m()); ++k) w[k] = io.aset[(int64_t)k * io.S + sc];
+    PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
+        const uint32_t v = (w[(2 * j) >> 5] >> ((2 * j) & 31)) & 3u;
+        bool fr = !PT::fixed(j) && v == 0u;
+        bool upj = !PT::fixed(j) && v == 2u;
+        if (upj && !PT::ufin(j)) { upj = false; fr = true; }
+        if (!fr && !upj && !PT::lfin(j) && !PT::fixed(j)) fr = true;
+        a.setF(j, fr);
+        a.setUp(j, upj);
+    }
+    PHX_UNROLL for (int i = 0; i < PT::m(); ++i) {
+        const int b = 2 * (PT::n() + i);
+        const uint32_t v = (w[b >> 5] >> (b & 31)) & 3u;
+        a.setR(i, PT::eq(i) || (v == 1u && PT::blfin(i)) || (v == 2u && PT::bufin(i)));
+        a.setLo(i, PT::eq(i) || v == 1u);
+    }
+}
+
+template <class PT>
+PHX_LD void aset_store(const LaneIO& io, int sc, const ASet<PT>& a) {
+    constexpr int NW = aset_words(PT::NMAX_N, PT::NMAX_M);
+    uint32_t w[NW];
+    PHX_UNROLL for (int k = 0; k < NW; ++k) w[k] = 0u;
+    PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
+        const uint32_t v = a.F(j) ? 0u : (a.up(j) ? 2u : 1u);
+        w[(2 * j) >> 5] |= v << ((2 * j) & 31);
+    }
+    PHX_UNROLL for (int i = 0; i < PT::m(); ++i) {
+        const int b = 2 * (PT::n() + i);
+        const uint32_t v = a.R(i) ? (a.lo(i) ? 1u : 2u) : 0u;
+        w[b >> 5] |= v << (b & 31);
+    }
+    PHX_UNROLL for (int k = 0; k < aset_words(PT::n(), PT::m()); ++k) io.aset[(int64_t)k * io.S + sc] = w[k];
+}
+
+// Classify at an interior-point (x, y): a bound/row is active when its slack
+// is within tol (relative) or smaller than its correctly-signed multiplier
+// (OSQP's polish rule, sharp at IPM points by strict complementarity).
+template <class PT>
+PHX_LD void classify(const Data<PT>& D, const double* xv, const double* yv, double tol, ASet<PT>& a) {
+    double aty[PT::NMAX_N];
+    D.matvec_t(yv, aty);
+    PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
+        const double lam = D.q(j) + D.p(j) * xv[j] - aty[j];
+        bool fr = !PT::fixed(j), upj = false;
+        if (fr && PT::lfin(j)) {
+            const double lo = D.l(j);
+            if (xv[j] - lo <= tol * (1.0 + fabs(lo)) || xv[j] - lo < lam) fr = false;
+        }
+        if (fr && PT::ufin(j)) {
+            const double hi = D.u(j);
+            if (hi - xv[j] <= tol * (1.0 + fabs(hi)) || hi - xv[j] < -lam) { fr = false; upj = true; }
+        }
+        a.setF(j, fr);
+        a.setUp(j, upj);
+    }
+    double ax[PT::NMAX_M];
+    D.matvec(xv, ax);
+    PHX_UNROLL for (int i = 0; i < PT::m(); ++i) {
+        bool lo_act = PT::eq(i), up_act = false;
+        if (!lo_act && PT::blfin(i)) {
+            const double lo = D.bl(i);
+            lo_act = ax[i] - lo <= tol * (1.0 + fabs(lo)) || ax[i] - lo < yv[i];
+        }
+        if (!lo_act && PT::bufin(i)) {
+            const double hi = D.bu(i);
+            up_act = hi - ax[i] <= tol * (1.0 + fabs(hi)) || hi - ax[i] < -yv[i];
+        }
+        a.setR(i, lo_act || up_act);
+        a.setLo(i, lo_act);
+    }
+}
+
+// Equality-constrained KKT solve for the active set a:
+//      [ P_FF   A_RF' ] [x_F]   [ -q_F        ]
+//      [ A_RF   0     ] [ z ] = [ b_R - A_RB x_B ]     (z = -y_R)
+// by its quasi-definite regularisation (P+reg, -reg) and iterative refinement
+// from the given (xp, z) (a proximal-point iteration that converges to the
+// KKT solution nearest the start on degenerate faces).  Non-free columns are
+// set to their bound.  false if the Schur complement is not positive definite.
+template <class PT>
+PHX_LD bool kkt_solve(const Data<PT>& D, const ASet<PT>& a, double* xp, double* z) {
+    constexpr int NN = PT::NMAX_N, MM = PT::NMAX_M, TT = PT::NMAX_M * (PT::NMAX_M + 1) / 2;
+    constexpr double reg = KKT_REG;
+    // 1/(p_j + reg): a literal for columns without a PH slot (p = 0), three
+    // or so reciprocals for the nonant columns; masked by F(j) where needed
+    double ipn[PT::NMAX_S];
+    PHX_UNROLL for (int j = 0; j < PT::n(); ++j)
+        if (PT::col_slot(j) >= 0) ipn[PT::col_slot(j)] = 1.0 / (D.p(j) + reg);
+    auto Hinv = [&](int j) { return PT::col_slot(j) >= 0 ? ipn[PT::col_slot(j)] : 1.0 / reg; };
+    double M[TT], idg[MM];
+    PHX_UNROLL for (int j = 0; j < PT::n(); ++j)
+        if (!a.F(j)) xp[j] = a.up(j) ? D.u(j) : D.l(j);
+    PHX_UNROLL for (int i = 0; i < PT::m(); ++i) if (!a.R(i)) z[i] = 0.0;
+    PHX_UNROLL for (int t = 0; t < TT; ++t) M[t] = 0.0;
+    PHX_UNROLL for (int i = 0; i < PT::m(); ++i) M[tri(i, i)] = a.R(i) ? reg : 1.0;
+    PHX_UNROLL for (int t = 0; t < PT::npairs(); ++t) {
+        const int ka = PT::pair_a(t), kb = PT::pair_b(t);
+        if (a.R(PT::row(ka)) && a.R(PT::row(kb)) && a.F(PT::col(ka)))
+            M[PT::pair_pos(t)] += D.A(ka) * Hinv(PT::col(ka)) * D.A(kb);
+    }
+    if (!cholesky<PT>(M, idg)) { PHX_LANE_FAIL(10, -1); return false; }
+    PHX_UNROLL for (int it = 0; it < KKT_REFINE; ++it) {
+        double r1[NN], t[MM];
+        {
+            double atz[NN];
+            D.matvec_t(z, atz);
+            PHX_UNROLL for (int j = 0; j < PT::n(); ++j)
+                r1[j] = a.F(j) ? -D.q(j) - D.p(j) * xp[j] - atz[j] : 0.0;
+        }
+        {
+            double axp[MM], hr[NN], ahr[MM];
+            D.matvec(xp, axp);
+            PHX_UNROLL for (int j = 0; j < PT::n(); ++j) hr[j] = r1[j] * Hinv(j);   // r1 = 0 off F
+            D.matvec(hr, ahr);
+            PHX_UNROLL for (int i = 0; i < PT::m(); ++i)
+                t[i] = a.R(i) ? ahr[i] - ((a.lo(i) ? D.bl(i) : D.bu(i)) - axp[i]) : 0.0;
+        }
+        chol_solve_inv<PT>(M, idg, t);
+        double atdz[NN];
+        D.matvec_t(t, atdz);
+        double dmax = 0.0, xmax = 0.0;
+        PHX_UNROLL for (int j = 0; j < PT::n(); ++j)
+            if (a.F(j)) {
+                const double d = (r1[j] - atdz[j]) * Hinv(j);
+                xp[j] += d;
+                dmax = fmax(dmax, fabs(d));
+                xmax = fmax(xmax, fabs(xp[j]));
+            }
+        PHX_UNROLL for (int i = 0; i < PT::m(); ++i)
+            if (a.R(i)) {
+                z[i] += t[i];
+                dmax = fmax(dmax, fabs(t[i]));
+                xmax = fmax(xmax, fabs(z[i]));
+            }
+        PHX_LANE_STAT(1);
+        if (dmax <= 1e-10 * (1.0 + xmax)) break;
+    }
+    return true;
+}
+
+// KKT certificate of (xp, z) for active set a (unscaled, relative kkt_tol);
+// on failure applies the primal-dual active-set update (violated bounds/rows
+// enter, wrong-signed multipliers leave).  Returns 0 certified, 1 active set
+// changed, 2 not certified and nothing to change.
+template <class PT>
+PHX_LD int certify_update(const Data<PT>& D, ASet<PT>& a, const double* xp, const double* z, double kkt_tol) {
+    double qmax = 0.0;
+    PHX_UNROLL for (int j = 0; j < PT::n(); ++j) qmax = fmax(qmax, fabs(D.q(j) * D.idc(j)));
+    const double dtol = kkt_tol * (1.0 + qmax);
+    const double ptol = kkt_tol;
+    bool ok = true, changed = false;
+    double atz[PT::NMAX_N];
+    D.matvec_t(z, atz);
+    PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
+        const double d = D.dc(j);
+        const double lam = (D.q(j) + D.p(j) * xp[j] + atz[j]) * D.idc(j);
+        if (a.F(j)) {
+            bool below = false, above = false;
+            if (PT::lfin(j)) {
+                const double lo = D.l(j);
+                below = xp[j] < lo && (lo - xp[j]) * d > ptol * (1.0 + fabs(lo * d));
+            }
+            if (PT::ufin(j)) {
+                const double hi = D.u(j);
+                above = xp[j] > hi && (xp[j] - hi) * d > ptol * (1.0 + fabs(hi * d));
+            }
+            if (below) { ok = false; changed = true; a.setF(j, false); a.setUp(j, false); PHX_LANE_FAIL(1, j); }
+            else if (above) { ok = false; changed = true; a.setF(j, false); a.setUp(j, true); PHX_LANE_FAIL(2, j); }
+            else if (fabs(lam) > dtol) { ok = false; PHX_LANE_FAIL(3, j); }
+        } else if (!PT::fixed(j)) {
+            if (!a.up(j) && lam < -dtol) { ok = false; changed = true; a.setF(j, true); PHX_LANE_FAIL(4, j); }
+            if (a.up(j) && lam > dtol) { ok = false; changed = true; a.setF(j, true); a.setUp(j, false); PHX_LANE_FAIL(5, j); }
+        }
+    }
+    double axp[PT::NMAX_M];
+    D.matvec(xp, axp);
+    PHX_UNROLL for (int i = 0; i < PT::m(); ++i) {
+        const double d = D.dr(i), id = D.idr(i);
+        bool below = false, above = false;
+        if (PT::blfin(i)) {
+            const double lo = D.bl(i);
+            below = axp[i] < lo && (lo - axp[i]) * id > ptol * (1.0 + fabs(lo * id));
+        }
+        if (PT::bufin(i)) {
+            const double hi = D.bu(i);
+            above = axp[i] > hi && (axp[i] - hi) * id > ptol * (1.0 + fabs(hi * id));
+        }
+        if (!a.R(i)) {
+            if (below) { ok = false; changed = true; a.setR(i, true); a.setLo(i, true); PHX_LANE_FAIL(6, i); }
+            else if (above) { ok = false; changed = true; a.setR(i, true); a.setLo(i, false); PHX_LANE_FAIL(7, i); }
+        } else {
+            if (below || above) { ok = false; PHX_LANE_FAIL(11, i); }
+            if (!PT::eq(i)) {
+                const double yy = -z[i] * d;
+                if (a.lo(i) && yy < -dtol) { ok = false; changed = true; a.setR(i, false); PHX_LANE_FAIL(8, i); }
+                if (!a.lo(i) && yy > dtol) { ok = false; changed = true; a.setR(i, false); PHX_LANE_FAIL(9, i); }
+            }
+        }
+    }
+    return ok ? 0 : (changed ? 1 : 2);
+}
+
+// KKT solve / certificate / active-set update rounds from (a, xp, z).
+template <class PT>
+PHX_LD bool as_rounds(const Data<PT>& D, ASet<PT>& a, const LaneIO& io, int rounds, double* xp, double* z) {
+#if defined(__HIPCC__) || defined(__HIPCC_RTC__)
+#pragma nounroll
+#endif
+    for (int r = 0; r < rounds; ++r) {
+        PHX_LANE_STAT(0);
+        if (!kkt_solve<PT>(D, a, xp, z)) return false;
+        const int c = certify_update<PT>(D, a, xp, z, io.kkt_tol);
+        if (c == 0) return true;
+        if (c == 2) return false;
+    }
+    return false;
+}
+
+// Certified lane: unscaled outputs, objective (incl. PH terms), active set.
+template <class PT>
+PHX_LD void write_certified(const LaneIO& io, const Data<PT>& D, int sc, const ASet<PT>& a, const double* xp,
+                            const double* z, int its) {
     const int S = io.S;
+    double f = io.kN[sc];
+    PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
+        const double xu = xp[j] * D.dc(j);
+        io.x_out[(int64_t)j * S + sc] = xu;
+        f += D.c(j) * xp[j];
+        if (PT::col_slot(j) >= 0) f += D.qn[PT::col_slot(j)] * xu + 0.5 * D.pn[PT::col_slot(j)] * xu * xu;
+    }
+    if (io.y_out)
+        PHX_UNROLL for (int i = 0; i < PT::m(); ++i) io.y_out[(int64_t)i * S + sc] = -z[i] * D.dr(i);
+    io.obj_out[sc] = f;
+    io.status[sc] = 1;
+    io.iters[sc] = its;
+    if (io.status_out) io.status_out[sc] = 1;
+    if (io.iters_out) io.iters_out[sc] = its;
+    io.flags[sc] = its > 0 ? (FLAG_WRITTEN | FLAG_IPM_TRIED) : FLAG_WRITTEN;
+    aset_store<PT>(io, sc, a);
+}
+
+// ---------------------------------------------------------------------------
+// Kernel bodies.  Both return true if the lane still needs the generic path.
+// ---------------------------------------------------------------------------
+template <class PT>
+PHX_LD bool warm_lane(const LaneIO& io, int sc) {
+    constexpr int NN = PT::NMAX_N, MM = PT::NMAX_M;
+    const Data<PT> D(io, sc);
+    ASet<PT> a;
+    aset_load<PT>(io, sc, a);
+    double xp[NN], z[MM];
+    PHX_UNROLL for (int j = 0; j < PT::n(); ++j) xp[j] = 0.0;
+    PHX_UNROLL for (int i = 0; i < PT::m(); ++i) z[i] = 0.0;
+    if (as_rounds<PT>(D, a, io, io.as_rounds, xp, z)) {
+        write_certified<PT>(io, D, sc, a, xp, z, 0);
+        return false;
+    }
+    io.status[sc] = 0;
+    io.flags[sc] = 0;
+    return true;
+}
+
+template <class PT>
+PHX_LD bool cold_lane(const LaneIO& io, int sc) {
+    constexpr int NN = PT::NMAX_N, MM = PT::NMAX_M;
+    const Data<PT> D(io, sc);
+    const int S = io.S;
+    double x[NN], y[MM];
+    int its = 0;
+    const double err = ipm_core<PT>(D, io.max_it, io.ipm_tol, x, y, &its);
+    io.flags[sc] = FLAG_IPM_TRIED;
+    if (err < 1e-4) {
+        ASet<PT> a;
+        classify<PT>(D, x, y, fmin(1e-4, fmax(1e-9, 10.0 * err)), a);
+        double xp[NN], z[MM];
+        PHX_UNROLL for (int j = 0; j < PT::n(); ++j) xp[j] = x[j];
+        PHX_UNROLL for (int i = 0; i < PT::m(); ++i) z[i] = a.R(i) ? -y[i] : 0.0;
+        if (as_rounds<PT>(D, a, io, io.as_rounds, xp, z)) {
+            write_certified<PT>(io, D, sc, a, xp, z, its > 0 ? its : 1);
+            return false;
+        }
+    }
+    // hand the IPM point to the generic PDHG path
     PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
         const int64_t o = (int64_t)j * S + sc;
         io.xT[o] = x[j]; io.x[o] = x[j]; io.x0[o] = x[j];
@@ -456,159 +853,23 @@ PHX_LD void ipm_lane(const LaneIO& io, int sc) {
         io.yT[o] = y[i]; io.y[o] = y[i]; io.y0[o] = y[i];
     }
     io.err[sc] = err;
-    io.iters[sc] = it;
+    io.iters[sc] = its;
     io.status[sc] = 0;
-    io.flags[sc] = io.flags[sc] | 1;
+    return true;
 }
 
-// ---------------------------------------------------------------------------
-// Polish kernel body: from (xT, yT) written by ipm_lane.  Returns 1 if the
-// certificate holds (then the polished point replaces xT/yT and the warm start).
-// ---------------------------------------------------------------------------
-template <class PT>
-PHX_LD int polish_lane(const LaneIO& io, int sc) {
-    constexpr int NN = PT::NMAX_N, MM = PT::NMAX_M, TT = PT::NMAX_M * (PT::NMAX_M + 1) / 2;
-    const double e = io.err[sc];
-    if (!(e < 1e-4)) { io.status[sc] = 0; return 0; }
-    const Data<PT> D(io, sc);
-    const int S = io.S;
-    const double tol = fmin(1e-4, fmax(1e-9, 10.0 * e));
-    const double reg = io.reg;
-    double xp[NN], z[MM];
-    bool F[NN], R[MM], lowside[MM];
-    {
-        double xv[NN], yv[MM];
-        PHX_UNROLL for (int j = 0; j < PT::n(); ++j) xv[j] = io.xT[(int64_t)j * S + sc];
-        PHX_UNROLL for (int i = 0; i < PT::m(); ++i) yv[i] = io.yT[(int64_t)i * S + sc];
-        double aty[NN];
-        D.matvec_t(yv, aty);
-        PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
-            const double lam = D.q(j) + D.p(j) * xv[j] - aty[j];
-            bool fr = true;
-            double v = xv[j];
-            if (PT::lfin(j)) {
-                const double lo = D.l(j);
-                if (xv[j] - lo <= tol * (1.0 + fabs(lo)) || xv[j] - lo < lam) { fr = false; v = lo; }
-            }
-            if (fr && PT::ufin(j)) {
-                const double hi = D.u(j);
-                if (hi - xv[j] <= tol * (1.0 + fabs(hi)) || hi - xv[j] < -lam) { fr = false; v = hi; }
-            }
-            F[j] = fr;
-            xp[j] = v;
-        }
-        double ax[MM];
-        D.matvec(xv, ax);
-        PHX_UNROLL for (int i = 0; i < PT::m(); ++i) {
-            bool lo_act = false, up_act = false;
-            if (PT::blfin(i)) {
-                const double lo = D.bl(i);
-                lo_act = ax[i] - lo <= tol * (1.0 + fabs(lo)) || ax[i] - lo < yv[i];
-            }
-            if (!lo_act && PT::bufin(i)) {
-                const double hi = D.bu(i);
-                up_act = hi - ax[i] <= tol * (1.0 + fabs(hi)) || hi - ax[i] < -yv[i];
-            }
-            R[i] = lo_act || up_act;
-            lowside[i] = lo_act;
-            z[i] = R[i] ? -yv[i] : 0.0;
-        }
-    }
-    double Dx[NN], M[TT];
-    PHX_UNROLL for (int j = 0; j < PT::n(); ++j) Dx[j] = F[j] ? 1.0 / (D.p(j) + reg) : 0.0;
-    PHX_UNROLL for (int t = 0; t < TT; ++t) M[t] = 0.0;
-    PHX_UNROLL for (int i = 0; i < PT::m(); ++i) M[tri(i, i)] = R[i] ? reg : 1.0;
-    PHX_UNROLL for (int t = 0; t < PT::npairs(); ++t) {
-        const int ka = PT::pair_a(t), kb = PT::pair_b(t);
-        if (R[PT::row(ka)] && R[PT::row(kb)]) M[PT::pair_pos(t)] += D.A(ka) * Dx[PT::col(ka)] * D.A(kb);
-    }
-    bool ok = cholesky<PT>(M);
-    if (ok) {
-        for (int it = 0; it < io.refine; ++it) {
-            double r1[NN], t[MM];
-            {
-                double atz[NN];
-                D.matvec_t(z, atz);
-                PHX_UNROLL for (int j = 0; j < PT::n(); ++j)
-                    r1[j] = F[j] ? -D.q(j) - D.p(j) * xp[j] - atz[j] : 0.0;
-            }
-            {
-                double axp[MM], hr[NN], ahr[MM];
-                D.matvec(xp, axp);
-                PHX_UNROLL for (int j = 0; j < PT::n(); ++j) hr[j] = r1[j] * Dx[j];
-                D.matvec(hr, ahr);
-                PHX_UNROLL for (int i = 0; i < PT::m(); ++i) {
-                    const double b = lowside[i] ? D.bl(i) : D.bu(i);
-                    t[i] = R[i] ? ahr[i] - (b - axp[i]) : 0.0;
-                }
-            }
-            chol_solve<PT>(M, t);
-            double atdz[NN];
-            D.matvec_t(t, atdz);
-            PHX_UNROLL for (int j = 0; j < PT::n(); ++j)
-                if (F[j]) xp[j] += (r1[j] - atdz[j]) * Dx[j];
-            PHX_UNROLL for (int i = 0; i < PT::m(); ++i)
-                if (R[i]) z[i] += t[i];
-        }
-        // certificate (unscaled, relative kkt_tol)
-        double qmax = 0.0;
-        PHX_UNROLL for (int j = 0; j < PT::n(); ++j) qmax = fmax(qmax, fabs(D.q(j) / D.dc(j)));
-        const double dtol = io.kkt_tol * (1.0 + qmax);
-        const double ptol = io.kkt_tol;
-        {
-            double atz[NN];
-            D.matvec_t(z, atz);
-            PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
-                const double d = D.dc(j);
-                if (PT::lfin(j)) {
-                    const double lo = D.l(j);
-                    if (xp[j] < lo && (lo - xp[j]) * d > ptol * (1.0 + fabs(lo * d))) ok = false;
-                }
-                if (PT::ufin(j)) {
-                    const double hi = D.u(j);
-                    if (xp[j] > hi && (xp[j] - hi) * d > ptol * (1.0 + fabs(hi * d))) ok = false;
-                }
-                const double lam = (D.q(j) + D.p(j) * xp[j] + atz[j]) / d;
-                if (F[j]) {
-                    if (fabs(lam) > dtol) ok = false;
-                } else if (!PT::fixed(j)) {
-                    const bool atl = PT::lfin(j) && (xp[j] == D.l(j));
-                    if (atl && lam < -dtol) ok = false;
-                    if (!atl && lam > dtol) ok = false;
-                }
-            }
-        }
-        double axp[MM];
-        D.matvec(xp, axp);
-        PHX_UNROLL for (int i = 0; i < PT::m(); ++i) {
-            const double d = D.dr(i);
-            if (PT::blfin(i)) {
-                const double lo = D.bl(i);
-                if (axp[i] < lo && (lo - axp[i]) / d > ptol * (1.0 + fabs(lo / d))) ok = false;
-            }
-            if (PT::bufin(i)) {
-                const double hi = D.bu(i);
-                if (axp[i] > hi && (axp[i] - hi) / d > ptol * (1.0 + fabs(hi / d))) ok = false;
-            }
-            if (R[i] && !PT::eq(i)) {
-                const double yy = -z[i] * d;
-                if (lowside[i] && yy < -dtol) ok = false;
-                if (!lowside[i] && yy > dtol) ok = false;
-            }
-        }
-    }
-    io.status[sc] = ok ? 1 : 0;
-    if (ok) {
-        PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
-            const int64_t o = (int64_t)j * S + sc;
-            io.xT[o] = xp[j]; io.x[o] = xp[j]; io.x0[o] = xp[j];
-        }
-        PHX_UNROLL for (int i = 0; i < PT::m(); ++i) {
-            const int64_t o = (int64_t)i * S + sc;
-            io.yT[o] = -z[i]; io.y[o] = -z[i]; io.y0[o] = -z[i];
-        }
-    }
-    return ok ? 1 : 0;
+#if defined(__HIPCC__) || defined(__HIPCC_RTC__)
+// Compact the lanes that still need work into out[0..*count): one atomic per
+// wavefront, lane order kept within the wavefront.  Every lane of the
+// wavefront must reach this call.
+__device__ __forceinline__ void compact_lane(bool still, int sc, int32_t* out, int32_t* count) {
+    const unsigned long long b = __ballot(still);
+    const int lane = threadIdx.x & 63;
+    int base = 0;
+    if (lane == 0 && b) base = atomicAdd(count, (int32_t)__popcll(b));
+    base = __shfl(base, 0, 64);
+    if (still) out[base + __popcll(b & ((1ull << lane) - 1ull))] = sc;
 }
+#endif
 
 }  // namespace phx_lane

@@ -100,10 +100,6 @@ class PHBase(SPOpt):
                                       self._partial.data_ptr(), self._node_buf.data_ptr(), self._stream()),
                   "xbar")
         self.mpicomm.allreduce_(self._node_buf)
-        NNS = self.NNS
-        if NNS:
-            self._xbar_node.copy_(self._node_buf[:NNS])
-            self._xsqbar_node.copy_(self._node_buf[NNS:2 * NNS])
         self._conv_cache = None
         self._bump()
         if verbose and self.cylinder_rank == 0:
@@ -113,10 +109,11 @@ class PHBase(SPOpt):
         lib = self._native
         lib.check(self._ctx, lib.update_w(self._ctx, self._x.data_ptr(), self._xbar_node.data_ptr(),
                                           self._xbar_idx_t.data_ptr(), self._rho.data_ptr(),
-                                          self._W.data_ptr(), int(update), self._dsum.data_ptr(),
+                                          self._W.data_ptr(), int(update), None,
                                           self._conv_R, self._seg_s0, self._seg_s1,
                                           self._seg_sums.data_ptr(), self._stream()), "update_w")
-        self._conv_cache = self._seg_sums.clone()
+        self._conv_cache = self._seg_sums      # consumed (all-reduced) by convergence_diff
+        self._conv_value = None
         self._bump()
 
     def Update_W(self, verbose):
@@ -129,15 +126,17 @@ class PHBase(SPOpt):
         """(1/R) sum_r mean_{(s,i) in rank r} |x - xbar|  (phbase.py:321-343)."""
         if getattr(self, "_conv_cache", None) is None:
             self._update_w_and_diff(False)
-        t = self._conv_cache.clone()
-        self.mpicomm.allreduce_(t)
-        v = t.cpu().numpy()
-        cnt = self._conv_counts
-        tot = 0.0
-        for r in range(self._conv_R):
-            if cnt[r] > 0:
-                tot += v[r] / cnt[r]
-        return tot / self._conv_R
+        if getattr(self, "_conv_value", None) is None:
+            t = self._conv_cache
+            self.mpicomm.allreduce_(t)
+            v = t.cpu().numpy()
+            cnt = self._conv_counts
+            tot = 0.0
+            for r in range(self._conv_R):
+                if cnt[r] > 0:
+                    tot += v[r] / cnt[r]
+            self._conv_value = tot / self._conv_R
+        return self._conv_value
 
     def _populate_W_cache(self, cache, padding):
         """Flat scenario-major W export (phbase.py:346-366)."""

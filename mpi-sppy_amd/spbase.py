@@ -221,7 +221,7 @@ class SPBase:
             xbar_idx[j] = node_off[node_id[t]] + nn.slot_local[j]
         self._xbar_idx = xbar_idx
         # tiles for the segmented xbar reduction
-        CH = int(self.options.get("xbar_tile", 8192))
+        CH = int(self.options.get("xbar_tile", 1024))
         slot_lo = [int(np.argmax(nn.slot_stage == t + 1)) for t in range(T)]
         tiles = []   # (node v, s0, s1, slot0, nlen)
         for t in range(T):
@@ -293,15 +293,20 @@ class SPBase:
         self._x = torch.zeros(n * S, dtype=f64, device=self.device)
         self._y = torch.zeros(max(m, 1) * S, dtype=f64, device=self.device)
         self._obj = torch.zeros(S, dtype=f64, device=self.device)
-        self._outer = torch.zeros(S, dtype=f64, device=self.device)
+        # the batched solve is exact (KKT-certified), so each scenario's outer
+        # bound is its optimal objective (spopt.py:201-206): one buffer
+        self._outer = self._obj
         self._status = torch.zeros(S, dtype=i32, device=self.device)
         self._iters = torch.zeros(S, dtype=i32, device=self.device)
         self._prob = self._t(b.prob, f64)
         self._pc = self._t(self._prob_coeff.ravel(), f64)
         self._xbar_idx_t = self._t(self._xbar_idx.ravel(), i32)
-        self._xbar_node = torch.zeros(max(self.NNS, 1), dtype=f64, device=self.device)
-        self._xsqbar_node = torch.zeros(max(self.NNS, 1), dtype=f64, device=self.device)
-        self._node_buf = torch.zeros(max(2 * self.NNS, 1), dtype=f64, device=self.device)
+        # [sum p x | sum p x^2] per (node, slot), all-reduced in place; xbar and
+        # xsqbar are views of it (no copies per iteration)
+        self._node_buf = torch.zeros(max(2 * self.NNS, 2), dtype=f64, device=self.device)
+        NNS1 = max(self.NNS, 1)
+        self._xbar_node = self._node_buf[:NNS1]
+        self._xsqbar_node = self._node_buf[NNS1:2 * NNS1]
         self._dsum = torch.zeros(S, dtype=f64, device=self.device)
         self._seg_sums = torch.zeros(self._conv_R, dtype=f64, device=self.device)
         self._expect_buf = torch.zeros(3, dtype=f64, device=self.device)
@@ -334,6 +339,7 @@ class SPBase:
         tree.node_tile_ptr, tree.node_off, tree.node_nlen = td["ptr"].data_ptr(), td["noff"].data_ptr(), td["nl"].data_ptr()
         tree.NNS = self.NNS
         tree.npart = o
+        tree.nnodes_cover = int(sum(int(self._node_nlen[v]) for v in node_ids))
         self._tree = tree
         self._tree_t = td
         segs = self._conv_seg

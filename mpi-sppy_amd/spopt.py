@@ -13,7 +13,7 @@ passes solver options (``iter0_solver_options`` / ``iterk_solver_options``,
 phbase.py:273-275): keys ``pdhg_max_iters``, ``pdhg_check_every``,
 ``pdhg_restart_max``, ``polish``, ``polish_refine``, ``polish_below``,
 ``kkt_tol``, ``opt_tol``, ``polish_reg``, ``warm_start``, ``ipm_after``,
-``ipm_max_it``, ``ipm_tol``, ``lane_solver``.
+``ipm_max_it``, ``ipm_tol``, ``lane_solver``, ``as_rounds``.
 """
 import ctypes
 import inspect
@@ -40,6 +40,7 @@ SOLVER_DEFAULTS = {
     "ipm_max_it": 60,
     "ipm_tol": 1e-10,
     "lane_solver": 1,
+    "as_rounds": 4,
 }
 
 OPTIMAL, ITER_LIMIT, NUMERIC_FAIL = 1, 2, 3
@@ -96,6 +97,7 @@ class SPOpt(SPBase):
         so.ipm_max_it = int(o["ipm_max_it"])
         so.ipm_tol = float(o["ipm_tol"])
         so.lane_solver = int(o["lane_solver"])
+        so.as_rounds = int(o["as_rounds"])
         return so
 
     def _set_ph_terms(self):
@@ -125,16 +127,16 @@ class SPOpt(SPBase):
         lib.check(self._ctx, lib.solve(self._ctx, ctypes.byref(so), self._x.data_ptr(), self._y.data_ptr(),
                                        self._obj.data_ptr(), self._status.data_ptr(), self._iters.data_ptr(),
                                        ctypes.byref(total), self._stream()), "solve")
-        self._outer.copy_(self._obj)
         self._conv_cache = None
         self._bump()
         stt = _native.SolveStats()
         lib.check(self._ctx, lib.last_solve_stats(self._ctx, ctypes.byref(stt)), "last_solve_stats")
         st = self._status
-        n_bad = int((st != OPTIMAL).sum().item())
+        n_bad = int(stt.not_optimal)
         self.solve_stats.append({"pdhg_iters": int(total.value), "pdhg_ms": stt.pdhg_ms, "launches": stt.pdhg_launches,
                                  "lane_iters": stt.lane_iters, "polish_ms": stt.polish_ms, "ipm_ms": stt.ipm_ms,
-                                 "lane_ms": stt.lane_ms, "lane_polish_ms": stt.lane_polish_ms, "lane_certified": stt.lane_certified,
+                                 "lane_ms": stt.lane_ms, "lane_warm_ms": stt.lane_warm_ms, "lane_certified": stt.lane_certified,
+                                 "lane_warm_certified": stt.lane_warm_certified,
                                  "wall_s": time.perf_counter() - t0, "not_optimal": n_bad})
         if n_bad and gripe:
             stc = st.cpu().numpy()

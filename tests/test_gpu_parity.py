@@ -52,3 +52,47 @@ def test_aircond_multistage_vs_oracle(gpu_lib):
     assert rel(tb, otb) < 1e-9
     assert rel(Eobj, oE) < 1e-8
     assert rel(ph.W_array(), o.W) < 1e-7
+
+
+def test_lane_and_generic_paths_agree(gpu_lib):
+    """The structure-specialised lane solver (warm active set + IPM) and the
+    generic PDHG + polish path give the same PH trajectory."""
+    S = 200
+    res = []
+    for so in ({"lane_solver": 1}, {"lane_solver": 0}, {"lane_solver": 1, "as_rounds": 0}):
+        ph, conv, Eobj, tb = run_engine(farmer.scenario_creator, farmer.scenario_names_creator(S),
+                                        {"num_scens": S}, 4, lib=gpu_lib,
+                                        options={"iter0_solver_options": so, "iterk_solver_options": so})
+        assert all(s["not_optimal"] == 0 for s in ph.solve_stats)
+        res.append((ph.W_array(), ph.xbar_by_node()["ROOT"][0], Eobj, tb))
+    for W, xb, E, t in res[1:]:
+        assert rel(W, res[0][0]) < 1e-8
+        assert rel(xb, res[0][1]) < 1e-9
+        assert rel(E, res[0][2]) < 1e-9 and rel(t, res[0][3]) < 1e-9
+
+
+def test_farmer_100k_sampled_oracle(gpu_lib):
+    """Full-size run (BASELINE configs[2]: farmer, 100,000 scenarios): every
+    subproblem certified; a sample of scenarios re-solved by the CPU oracle
+    from the engine's own W / xbar agrees to 1e-6 relative (north_star bar)."""
+    S = 100000
+    ph, conv, Eobj, tb = run_engine(farmer.scenario_creator, farmer.scenario_names_creator(S),
+                                    {"num_scens": S}, 3, lib=gpu_lib)
+    assert all(s["not_optimal"] == 0 for s in ph.solve_stats)
+    W = ph.W_array()
+    xb = ph.xbar_by_node()["ROOT"][0]
+    xn = ph.nonant_values()
+    obj = ph._host("obj")
+    rng = np.random.RandomState(7)
+    sample = sorted(set(rng.randint(0, S, 48).tolist()) | {0, 1, 2, S - 1})
+    # W/xbar are those of the last update; the last solve used W, xbar after
+    # iteration 3's update, which are exactly the current values
+    scens = [om.farmer("scen%d" % k, num_scens=S) for k in sample]
+    o = oph.OraclePH(scens, rho=1.0)
+    o.W_on = o.prox_on = 1
+    o.W[:] = W[sample]
+    o.xbar[:] = xb[None, :]
+    o.solve_loop()
+    assert rel(o.xn(), xn[sample]) < 1e-6
+    assert rel(o.obj, obj[sample]) < 1e-8
+    assert 0.0 < conv < 1e4 and np.isfinite(Eobj) and np.isfinite(tb)
