@@ -5,21 +5,28 @@ convergence_diff -> batched subproblem solve), i.e. the body of
 ``PHBase.iterk_loop`` (mpisppy/phbase.py:901-970).  Workload: farmer,
 crops_multiplier 1, 100,000 synthetic scenarios (configs[2] of BASELINE.json;
 the metric is quoted on it and it fits one MI355X), rho = 1, scenarios sharded
-contiguously over the ranks (strong scaling: total scenarios fixed).
+contiguously over the ranks (strong scaling: the 100k total is fixed).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--scens S] [--cm C]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
 
 Timed region: K steps bracketed by barrier + device synchronize; the MAX over
-ranks is reported.  Iter0 and W warmup steps are untimed.  Inputs are resident
-in HBM before timing.  Extra keys: roofline (dominant kernel k_chunk, HIP
-event timing, algorithmic bytes per DESIGN.md §4), cpu_baseline (the CPU
-oracle — numpy + scipy HiGHS — on a bounded sample, rank 0, N=1 only),
-conv_time (time to conv < 1e-4 when --conv is given).
+ranks is reported.  Iter0 and the W warmup steps are untimed.  Inputs are
+resident in HBM before timing.  Extra keys:
+  roofline      the dominant kernel of the timed region (the structure-
+                specialised lane solver ``phx_lane_warm`` with the lane solver
+                on, the PDHG chunk ``k_chunk`` otherwise): algorithmic bytes
+                 / its average duration from HIP events recorded
+                on the solve stream inside phx_solve.
+  cpu_baseline  the CPU restatement of the reference PH (oracle/cpu_bench.py:
+                numpy + scipy-HiGHS + polish, one worker process per core) on a
+                bounded sample, run as a child process on rank 0 at N = 1.
+  conv_time     (--conv) wall time from Iter0 to conv < 1e-4.
 """
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -36,49 +43,72 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--scens", type=int, default=100000)
     ap.add_argument("--cm", type=int, default=1)
     ap.add_argument("--rho", type=float, default=1.0)
     ap.add_argument("--check-every", type=int, default=64)
     ap.add_argument("--ipm-after", type=int, default=None, help="PDHG iterations before the IPM finisher")
-    ap.add_argument("--lane-solver", type=int, default=1, help="1: structure-specialised lane IPM first")
+    ap.add_argument("--lane-solver", type=int, default=1, help="1: structure-specialised lane solver first")
+    ap.add_argument("--as-rounds", type=int, default=None, help="active-set rounds (0: no warm active set)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=400)
+    ap.add_argument("--cpu-scens", type=int, default=4000)
+    ap.add_argument("--cpu-iters", type=int, default=3)
+    ap.add_argument("--cpu-procs", type=int, default=16, help="worker processes (the GPU box's CPU share)")
     ap.add_argument("--conv", action="store_true", help="also measure time to conv < 1e-4")
-    ap.add_argument("--conv-max-iters", type=int, default=3000)
+    ap.add_argument("--conv-max-iters", type=int, default=5000)
     return ap.parse_args()
 
 
-def bytes_per_lane_iter(b):
-    """Algorithmic bytes of one PDHG iteration of one scenario in k_chunk.
+def lane_bytes(b):
+    """Algorithmic HBM bytes of phx_lane_warm per scenario.
 
-    SpMM pair with de-duplicated A values:
-        8 * (2*nnz_var + 2*n + 2*m)
-    plus the fused vector updates of the iteration:  8 * (7*n + 5*m).
+    reads : varying A values, the PH terms qN/pN/kN, the active-set words,
+            plus c / bounds / row bounds where they vary by scenario
+    writes: x (n), row duals y (m), objective, status + iteration count
+            (caller's and the context's), flags, active-set words
+    The scenario-invariant data are literals of the JIT-specialised kernel.
     """
+    nw = (2 * (b.n + b.m) + 31) // 32
+    rd = 8 * (b.nvar + 2 * b.nonant.N + 1) + 4 * nw
+    rd += 8 * b.n * int(b.c_vary) + 16 * b.n * int(b.bnd_vary) + 16 * b.m * int(b.rhs_vary)
+    wr = 8 * (b.n + b.m + 1) + 4 * 5 + 4 * nw
+    return rd + wr
+
+
+def pdhg_bytes(b):
+    """Algorithmic bytes of one PDHG iteration of one scenario in k_chunk:
+    the SpMM pair with de-duplicated A values
+    8*(2*nnz_var + 2*n + 2*m) plus the fused vector updates 8*(7n + 5m)."""
     return 8 * (2 * b.nvar + 2 * b.n + 2 * b.m) + 8 * (7 * b.n + 5 * b.m)
 
 
+def pmc_traffic(kernel, args):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
+    (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; scripts/pmc_summary.py).
+    Counters need their own profiler runs, so they are read from profiles/."""
+    import glob
+    if args.scens != 100000 or args.cm != 1:
+        return None, None
+    files = sorted(glob.glob(os.path.join(_ROOT, "profiles", "r*_pmc_%s.json" % kernel)))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    t = d.get("hbm_bytes_per_launch", {}).get("total")
+    return t, os.path.relpath(files[-1], _ROOT)
+
+
 def cpu_baseline(args):
-    """The CPU oracle (HiGHS + KKT polish, numpy PH) on a bounded sample."""
-    from oracle import models as om, ph as oph
-    S = args.cpu_sample
-    scens = [om.farmer("scen%d" % i, crops_multiplier=args.cm, num_scens=S) for i in range(S)]
-    o = oph.OraclePH(scens, rho=args.rho)
-    o.iter0()
-    K = 2
-    t0 = time.perf_counter()
-    for _ in range(K):
-        o.compute_xbar()
-        o.update_w()
-        o.convergence_diff()
-        o.solve_loop()
-    dt = time.perf_counter() - t0
-    return {"value": S * K / dt, "unit": "scenario-iterations/s", "cores": 1, "kind": "port",
-            "sample": "oracle PH (numpy + scipy-HiGHS 1.8 QP + KKT polish), farmer cm=%d, %d scenarios x %d "
-                      "PH iterations after Iter0, 1 core" % (args.cm, S, K)}
+    """oracle/cpu_bench.py in a child process (it never touches the GPU)."""
+    procs = max(1, min(args.cpu_procs, os.cpu_count() or 1))
+    cmd = [sys.executable, "-m", "oracle.cpu_bench", "--scens", str(args.cpu_scens), "--iters",
+           str(args.cpu_iters), "--procs", str(procs), "--cm", str(args.cm), "--rho", str(args.rho)]
+    r = subprocess.run(cmd, cwd=_ROOT, capture_output=True, text=True, timeout=600)
+    if r.returncode != 0:
+        return {"error": r.stderr[-500:]}
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    return {k: d[k] for k in ["value", "unit", "cores", "kind", "sample", "seconds"]}
 
 
 def main():
@@ -101,6 +131,8 @@ def main():
     solver_opts = {"pdhg_check_every": args.check_every, "lane_solver": args.lane_solver}
     if args.ipm_after is not None:
         solver_opts["ipm_after"] = args.ipm_after
+    if args.as_rounds is not None:
+        solver_opts["as_rounds"] = args.as_rounds
     opts = {"solver_name": "phx", "PHIterLimit": 10 ** 9, "defaultPHrho": args.rho, "convthresh": 1e-10,
             "verbose": False, "display_progress": False, "iter0_solver_options": dict(solver_opts),
             "iterk_solver_options": dict(solver_opts)}
@@ -138,23 +170,35 @@ def main():
     ph.mpicomm.allreduce_max_(dt_t)
     dt = float(dt_t.item())
     stats = ph.solve_stats[n0:]
-    pdhg_ms = sum(s["pdhg_ms"] for s in stats)
-    launches = sum(s["launches"] for s in stats)
-    lane_iters = sum(s["lane_iters"] for s in stats)
     b = ph.batch
-    bpl = bytes_per_lane_iter(b)
-    avg_launch_s = pdhg_ms / 1e3 / max(launches, 1)
-    bytes_per_launch = lane_iters * bpl / max(launches, 1)
+    K = args.steps
+    lane_on = any(s.get("lane_ms", 0.0) > 0.0 for s in stats)
+    if lane_on:
+        # dominant kernel: the warm active-set lane kernel, one launch per step over all local scenarios
+        k_ms = sum(s.get("lane_warm_ms", 0.0) for s in stats)
+        launches = sum(1 for s in stats if s.get("lane_warm_ms", 0.0) > 0.0)
+        bpu = lane_bytes(b)
+        units_per_launch = b.S
+        kernel = "phx_lane_warm"
+    else:
+        k_ms = sum(s["pdhg_ms"] for s in stats)
+        launches = sum(s["launches"] for s in stats)
+        bpu = pdhg_bytes(b)
+        units_per_launch = sum(s["lane_iters"] for s in stats) / max(launches, 1)
+        kernel = "k_chunk"
+    avg_launch_s = k_ms / 1e3 / max(launches, 1)
+    bytes_per_launch = bpu * units_per_launch
     achieved = bytes_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
-    value = S * args.steps / dt
+    value = S * K / dt
+    traffic, traffic_src = pmc_traffic(kernel, args) if world == 1 else (None, None)
     res = {
         "metric": "PH scenario-iterations/sec (farmer)",
         "value": value,
         "unit": "scenario-iterations/s",
         "n_gpus": world,
-        "steps": args.steps,
+        "steps": K,
         "warmup": args.warmup,
-        "ms_per_step": dt * 1e3 / args.steps,
+        "ms_per_step": dt * 1e3 / K,
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
@@ -162,25 +206,29 @@ def main():
         "data": "synthetic (farmer scenario generator, RandomState-seeded yields as the reference)",
         "config": {"workload": "farmer crops_multiplier=%d, %d scenarios, rho=%g, PH iterate" % (args.cm, S, args.rho),
                    "scenarios": S, "scenarios_per_gpu": b.S, "n": b.n, "m": b.m, "nnz": b.nnz,
-                   "nnz_varying": b.nvar, "parallelism": "scenario-sharded x%d, RCCL allreduce" % world},
+                   "nnz_varying": b.nvar, "nonants": b.nonant.N,
+                   "parallelism": "scenario-sharded x%d, RCCL allreduce" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "k_chunk", "bytes_per_scenario_iter": bpl,
-                     "avg_launch_us": avg_launch_s * 1e6, "launches": launches,
-                     "scenario_iters_per_launch": lane_iters / max(launches, 1)},
-        "pdhg_iters_per_step": [s["pdhg_iters"] for s in stats],
-        "kernel_ms_per_step": {"pdhg": pdhg_ms / args.steps, "polish": sum(s["polish_ms"] for s in stats) / args.steps,
-                               "ipm": sum(s["ipm_ms"] for s in stats) / args.steps,
-                               "lane_ipm": sum(s.get("lane_ms", 0.0) for s in stats) / args.steps,
-                               "lane_warm": sum(s.get("lane_warm_ms", 0.0) for s in stats) / args.steps},
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/launch",
+                     "traffic_source": traffic_src, "algorithmic_bytes_per_launch": bytes_per_launch,
+                     "kernel": kernel, "bytes_per_unit": bpu,
+                     "unit_def": "scenario solve" if lane_on else "scenario PDHG iteration",
+                     "units_per_launch": units_per_launch,
+                     "avg_launch_us": avg_launch_s * 1e6, "launches": launches},
+        "kernel_ms_per_step": {"lane_warm": sum(s.get("lane_warm_ms", 0.0) for s in stats) / K,
+                               "lane_cold": sum(s.get("lane_ms", 0.0) for s in stats) / K,
+                               "pdhg": sum(s["pdhg_ms"] for s in stats) / K,
+                               "polish": sum(s["polish_ms"] for s in stats) / K,
+                               "ipm": sum(s["ipm_ms"] for s in stats) / K},
         "lane_certified_per_step": [s.get("lane_certified") for s in stats],
         "lane_warm_certified_per_step": [s.get("lane_warm_certified") for s in stats],
+        "pdhg_iters_per_step": [s["pdhg_iters"] for s in stats],
         "solver_options": solver_opts,
         "not_optimal": sum(s["not_optimal"] for s in stats),
         "setup_s": t_setup, "iter0_s": t_iter0,
     }
     if args.conv:
-        # time to conv < 1e-4 from Iter0 (fresh object)
+        # time to conv < 1e-4 from Iter0 (fresh object, same data)
         del ph
         opts2 = dict(opts)
         opts2["convthresh"] = 1e-4
@@ -188,10 +236,13 @@ def main():
         ph2 = PH(opts2, names, farmer.scenario_creator,
                  scenario_creator_kwargs={"num_scens": S, "crops_multiplier": args.cm})
         torch.cuda.synchronize()
+        ph2.mpicomm.Barrier()
         t0 = time.perf_counter()
         ph2.ph_main(finalize=False)
         torch.cuda.synchronize()
-        res["conv_time"] = {"seconds": time.perf_counter() - t0, "iterations": ph2._PHIter,
+        tc = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
+        ph2.mpicomm.allreduce_max_(tc)
+        res["conv_time"] = {"seconds": float(tc.item()), "iterations": ph2._PHIter,
                             "conv": ph2.conv, "convthresh": 1e-4}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(args)

@@ -26,7 +26,7 @@ import torch
 
 from . import _native
 from . import batch as batchmod
-from .comm import Comm
+from .comm import Comm, init_from_env
 from .utils import sputils
 
 
@@ -64,7 +64,12 @@ class SPBase:
             raise NotImplementedError("variable_probability is not supported by the batched engine")
         self.variable_probability = None
         self.multistage = len(self.all_nodenames) > 1
-        self.mpicomm = mpicomm if mpicomm is not None else Comm()
+        if mpicomm is None:
+            # under torchrun (WORLD_SIZE > 1) join the process group: RCCL for GPU
+            # tensors, gloo when the caller runs the engine on CPU tensors
+            dev_type = "cuda" if _device is None else torch.device(_device).type
+            mpicomm = init_from_env(dev_type)
+        self.mpicomm = mpicomm
         self.cylinder_rank = self.mpicomm.Get_rank()
         self.n_proc = self.mpicomm.Get_size()
         self.global_rank = self.cylinder_rank

@@ -1,0 +1,102 @@
+"""CPU baseline for bench.py — TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).
+
+The reference's PH iterate as it runs under ``mpiexec -n P`` (one process per
+core, contiguous scenario slices ``range(int(r*S/P), int((r+1)*S/P))``,
+``utils/sputils.py:803-810``), restated with the oracle: each worker process
+owns its slice and solves its subproblems with scipy-HiGHS + KKT polish
+(``SPOpt.solve_loop``, ``spopt.py:226-307``); the parent plays the per-node
+Allreduce of ``_Compute_Xbar`` (``phbase.py:83-87``).  No Pyomo model layer, so
+this is FASTER than the reference itself: a conservative baseline.
+
+Timed: K PH iterations (Compute_Xbar -> Update_W -> convergence_diff ->
+solve_loop) after an untimed Iter0.  Prints one JSON line.
+
+    python -m oracle.cpu_bench --scens 4000 --iters 3 --procs 16
+
+Run by bench.py as a CHILD PROCESS (it never touches the GPU).
+"""
+import argparse
+import json
+import multiprocessing as mp
+import os
+import sys
+import time
+
+import numpy as np
+
+_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if _ROOT not in sys.path:
+    sys.path.insert(0, _ROOT)
+
+from oracle import models as om, ph as oph  # noqa: E402
+
+
+def _worker(conn, names, S, cm, rho):
+    scens = [om.farmer(nm, crops_multiplier=cm, num_scens=S) for nm in names]
+    o = oph.OraclePH(scens, rho=rho)
+    o.iter0()
+    conn.send((o.xn(), o.obj.copy()))
+    while True:
+        msg = conn.recv()
+        if msg is None:
+            break
+        xbar = msg
+        o.xbar[:] = xbar[None, :]
+        o.update_w()
+        d = float(np.sum(np.abs(o.xn() - o.xbar)))
+        o.solve_loop()
+        conn.send((o.xn(), d))
+    conn.close()
+
+
+def run(S, K, P, cm=1, rho=1.0):
+    names = ["scen%d" % i for i in range(S)]
+    avg = S / P
+    slices = [names[int(r * avg):int((r + 1) * avg)] for r in range(P)]
+    ctx = mp.get_context("fork")
+    pipes, procs = [], []
+    t_setup = time.perf_counter()
+    for sl in slices:
+        a, b = ctx.Pipe()
+        p = ctx.Process(target=_worker, args=(b, sl, S, cm, rho))
+        p.start()
+        pipes.append(a)
+        procs.append(p)
+    res = [c.recv() for c in pipes]          # Iter0 done everywhere
+    t_setup = time.perf_counter() - t_setup
+    prob = 1.0 / S
+    xn = np.concatenate([r[0] for r in res])
+    t0 = time.perf_counter()
+    conv = None
+    for _ in range(K):
+        xbar = prob * xn.sum(axis=0)         # Compute_Xbar (+ the Allreduce)
+        for c in pipes:
+            c.send(xbar)
+        res = [c.recv() for c in pipes]
+        xn = np.concatenate([r[0] for r in res])
+        conv = sum(r[1] for r in res) / (S * xn.shape[1])
+    dt = time.perf_counter() - t0
+    for c in pipes:
+        c.send(None)
+    for p in procs:
+        p.join()
+    return {"value": S * K / dt, "unit": "scenario-iterations/s", "cores": P, "kind": "port",
+            "seconds": dt, "setup_and_iter0_seconds": t_setup, "conv_last": conv,
+            "sample": "oracle PH restatement (numpy + scipy-HiGHS 1.8 LP/QP + KKT polish), farmer cm=%d, %d "
+                      "scenarios x %d PH iterations after Iter0, %d worker processes (contiguous slices, "
+                      "parent = Allreduce)" % (cm, S, K, P)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scens", type=int, default=4000)
+    ap.add_argument("--iters", type=int, default=3)
+    ap.add_argument("--procs", type=int, default=min(16, os.cpu_count() or 1))
+    ap.add_argument("--cm", type=int, default=1)
+    ap.add_argument("--rho", type=float, default=1.0)
+    a = ap.parse_args()
+    print(json.dumps(run(a.scens, a.iters, a.procs, a.cm, a.rho)), flush=True)
+
+
+if __name__ == "__main__":
+    main()
