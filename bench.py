@@ -64,14 +64,15 @@ def parse():
 def lane_bytes(b):
     """Algorithmic HBM bytes of phx_lane_warm per scenario.
 
-    reads : varying A values, the PH terms qN/pN/kN, the active-set words,
-            plus c / bounds / row bounds where they vary by scenario
+    reads : varying A values, W and rho of the nonant slots with their x-bar
+            index (x-bar itself is a per-node vector, cache-resident), the
+            active-set words, plus c / bounds / row bounds where they vary
     writes: x (n), row duals y (m), objective, status + iteration count
             (caller's and the context's), flags, active-set words
     The scenario-invariant data are literals of the JIT-specialised kernel.
     """
     nw = (2 * (b.n + b.m) + 31) // 32
-    rd = 8 * (b.nvar + 2 * b.nonant.N + 1) + 4 * nw
+    rd = 8 * (b.nvar + 2 * b.nonant.N) + 4 * b.nonant.N + 4 * nw
     rd += 8 * b.n * int(b.c_vary) + 16 * b.n * int(b.bnd_vary) + 16 * b.m * int(b.rhs_vary)
     wr = 8 * (b.n + b.m + 1) + 4 * 5 + 4 * nw
     return rd + wr
@@ -216,6 +217,7 @@ def main():
                      "units_per_launch": units_per_launch,
                      "avg_launch_us": avg_launch_s * 1e6, "launches": launches},
         "kernel_ms_per_step": {"lane_warm": sum(s.get("lane_warm_ms", 0.0) for s in stats) / K,
+                               "lane_warm_list": sum(s.get("lane_warm_list_ms", 0.0) for s in stats) / K,
                                "lane_cold": sum(s.get("lane_ms", 0.0) for s in stats) / K,
                                "pdhg": sum(s["pdhg_ms"] for s in stats) / K,
                                "polish": sum(s["polish_ms"] for s in stats) / K,

@@ -81,9 +81,14 @@ typedef struct phx_solve_opts {
     int32_t lane_solver;      /* 1: run the register-resident, structure-
                                  specialised lane solver (IPM + polish) first
                                  when the context has one (small subproblems) */
-    int32_t as_rounds;        /* active-set rounds per lane-solver kernel; 0
-                                 disables the warm active-set pass (each solve
-                                 then starts with the interior point)        */
+    int32_t as_rounds;        /* active-set rounds of the warm pass and after
+                                 the interior point; 0 disables the warm
+                                 start (each solve starts with the interior
+                                 point)                                       */
+    int32_t warm_passes;      /* 1 (default): one warm pass over all lanes with
+                                 as_rounds rounds in-kernel; k > 1: k passes of
+                                 one round each, passes 2..k over the
+                                 compacted lanes whose active set changed    */
 } phx_solve_opts;
 
 /* Statistics of the most recent phx_solve (HIP events on the solve stream). */
@@ -92,7 +97,9 @@ typedef struct phx_solve_stats {
     double  polish_ms;        /* summed k_polish time                         */
     double  ipm_ms;           /* generic interior-point finisher              */
     double  lane_ms;          /* specialised lane kernel: IPM + active set    */
-    double  lane_warm_ms;     /* specialised lane kernel: warm active set     */
+    double  lane_warm_ms;     /* specialised lane kernel: warm active set,
+                                 first pass (all lanes)                       */
+    double  lane_warm_list_ms;/* further warm passes over compacted lanes     */
     double  lane_iters;       /* PDHG scenario-iterations executed            */
     int32_t pdhg_launches;
     int32_t total_iters;      /* PDHG iterations of the batch loop            */

@@ -39,14 +39,14 @@ class SolveOpts(ctypes.Structure):
         ("polish_below", c_double), ("opt_tol", c_double), ("kkt_tol", c_double),
         ("reg", c_double),
         ("ipm_after", c_int32), ("ipm_max_it", c_int32), ("ipm_tol", c_double),
-        ("lane_solver", c_int32), ("as_rounds", c_int32),
+        ("lane_solver", c_int32), ("as_rounds", c_int32), ("warm_passes", c_int32),
     ]
 
 
 class SolveStats(ctypes.Structure):
     _fields_ = [
         ("pdhg_ms", c_double), ("polish_ms", c_double), ("ipm_ms", c_double), ("lane_ms", c_double),
-        ("lane_warm_ms", c_double),
+        ("lane_warm_ms", c_double), ("lane_warm_list_ms", c_double),
         ("lane_iters", c_double), ("pdhg_launches", c_int32), ("total_iters", c_int32),
         ("lane_certified", c_int32), ("lane_warm_certified", c_int32), ("not_optimal", c_int32), ("jit", c_int32),
     ]

@@ -24,11 +24,18 @@ namespace phx {
 struct LaneStructure {
     int n = 0, m = 0, nnz = 0, npairs = 0, nvar = 0, nslot = 0;
     bool c_vary = false, bnd_vary = false, rhs_vary = false;
+    // false (default): the lane solver works on the UNSCALED problem — exact
+    // KKT solves need no equilibration, and the +-1 / 0 entries of A, the
+    // bounds and the costs then fold into adds and moves instead of literal
+    // multiplies; dc/dr (the generic path's scaling) are kept only to hand a
+    // lane over to the scaled PDHG path.
+    bool scaled = false;
     std::vector<int32_t> row, col, kvar, col_slot;
     std::vector<int32_t> pair_a, pair_b, pair_pos;
     std::vector<uint8_t> lfin, ufin, fixed, blfin, bufin, eq;
-    // scaled scenario-invariant numbers, baked into the kernel as literals
-    // (c / lb,ub / bl,bu only when they do not vary across scenarios)
+    // scenario-invariant numbers (scaled iff `scaled`), baked into the kernel
+    // as literals (c / lb,ub / bl,bu only when they do not vary across
+    // scenarios); dc, dr: the generic path's column/row scaling
     std::vector<double> Ac, dc, dr, c, lb, ub, bl, bu;
 };
 
@@ -143,6 +150,7 @@ inline std::string lane_kernel_source(const LaneStructure& L, int warm_waves = 1
     o << "  static constexpr int NMAX_N = " << L.n << ", NMAX_M = " << L.m << ", NMAX_K = " << L.nnz
       << ", NMAX_V = " << std::max(L.nvar, 1) << ", NMAX_S = " << std::max(L.nslot, 1) << ";\n";
     o << "  __host__ __device__ static constexpr int nvar() { return " << L.nvar << "; }\n";
+    o << "  __host__ __device__ static constexpr bool scaled() { return " << (L.scaled ? "true" : "false") << "; }\n";
     o << "  __host__ __device__ static constexpr int nslot() { return " << L.nslot << "; }\n";
     o << "  __host__ __device__ static constexpr int n() { return " << L.n << "; }\n";
     o << "  __host__ __device__ static constexpr int m() { return " << L.m << "; }\n";
@@ -182,6 +190,10 @@ inline std::string lane_kernel_source(const LaneStructure& L, int warm_waves = 1
     emit_dtable(o, "bls", L.bl);
     emit_dtable(o, "bus", L.bu);
     o << "};\n";
+    // phx_lane_warm: one active-set round over every lane (the per-iteration
+    // pass); phx_lane_warm_list: one more round over a compacted lane list
+    // (the few lanes whose active set changed), so no wavefront idles while
+    // one of its lanes needs a second round.
     o << "extern \"C\" __global__ void __launch_bounds__(64, " << warm_waves
       << ") phx_lane_warm(phx_lane::LaneIO io) {\n"
          "  const int t = blockIdx.x * 64 + threadIdx.x;\n"
@@ -189,14 +201,27 @@ inline std::string lane_kernel_source(const LaneStructure& L, int warm_waves = 1
          "  if (t < io.S) still = phx_lane::warm_lane<PT>(io, t);\n"
          "  phx_lane::compact_lane(still, t, io.lanes_out, io.count_out);\n"
          "}\n";
+    o << "extern \"C\" __global__ void __launch_bounds__(64, " << warm_waves
+      << ") phx_lane_warm_list(phx_lane::LaneIO io, const int* lanes, const int* count) {\n"
+         "  const int nl = *count;\n"
+         "  for (int base = blockIdx.x * 64; base < nl; base += gridDim.x * 64) {\n"
+         "    const int t = base + threadIdx.x;\n"
+         "    bool still = false;\n"
+         "    int sc = -1;\n"
+         "    if (t < nl) { sc = lanes[t]; still = phx_lane::warm_lane<PT>(io, sc); }\n"
+         "    phx_lane::compact_lane(still, sc, io.lanes_out, io.count_out);\n"
+         "  }\n"
+         "}\n";
     o << "extern \"C\" __global__ void __launch_bounds__(64) phx_lane_cold(phx_lane::LaneIO io, "
          "const int* lanes, const int* count) {\n"
-         "  const int t = blockIdx.x * 64 + threadIdx.x;\n"
          "  const int nl = count ? *count : io.S;\n"
-         "  bool still = false;\n"
-         "  int sc = -1;\n"
-         "  if (t < nl) { sc = lanes ? lanes[t] : t; still = phx_lane::cold_lane<PT>(io, sc); }\n"
-         "  phx_lane::compact_lane(still, sc, io.lanes_out, io.count_out);\n"
+         "  for (int base = blockIdx.x * 64; base < nl; base += gridDim.x * 64) {\n"
+         "    const int t = base + threadIdx.x;\n"
+         "    bool still = false;\n"
+         "    int sc = -1;\n"
+         "    if (t < nl) { sc = lanes ? lanes[t] : t; still = phx_lane::cold_lane<PT>(io, sc); }\n"
+         "    phx_lane::compact_lane(still, sc, io.lanes_out, io.count_out);\n"
+         "  }\n"
          "}\n";
     return o.str();
 }

@@ -48,9 +48,18 @@ typedef unsigned long long uint64_t;
 #if defined(__HIPCC__) || defined(__HIPCC_RTC__)
 #define PHX_LD __host__ __device__ __forceinline__
 #define PHX_UNROLL _Pragma("unroll")
+#define PHX_NOUNROLL _Pragma("nounroll")
 #else
 #define PHX_LD inline
 #define PHX_UNROLL
+#define PHX_NOUNROLL
+#endif
+// Refinement loop: kept as a loop by default (the fully unrolled refinement
+// multiplies the straight-line code the instruction cache must stream).
+#ifdef PHX_REFINE_UNROLL
+#define PHX_REFINE_LOOP PHX_UNROLL
+#else
+#define PHX_REFINE_LOOP PHX_NOUNROLL
 #endif
 
 // Diagnostics hook (the CPU emulation defines it to record why a lane failed;
@@ -82,17 +91,23 @@ constexpr int32_t FLAG_IPM_TRIED = 1;   // interior point already attempted
 constexpr int32_t FLAG_WRITTEN = 2;     // outputs written by a lane kernel
 
 // Runtime inputs/outputs (device pointers; per-scenario arrays [i*S + s]).
+// A, c, bounds below are scaled iff PT::scaled() (phx_jit.h LaneStructure).
 struct LaneIO {
     int32_t S;
-    const double* Av;      // varying scaled A values [nvar*S]
-    const double* c;       // scaled c   [n*S] (only read if PT::c_vary())
-    const double* lb;      // scaled lb  [n*S] (PT::bnd_vary())
+    const double* Av;      // varying A values [nvar*S]
+    const double* c;       // c   [n*S] (only read if PT::c_vary())
+    const double* lb;      // lb  [n*S] (PT::bnd_vary())
     const double* ub;
-    const double* bl;      // scaled bl  [m*S] (PT::rhs_vary())
+    const double* bl;      // bl  [m*S] (PT::rhs_vary())
     const double* bu;
-    const double* qN;      // unscaled PH linear term [N*S]
-    const double* pN;      // unscaled PH quadratic   [N*S]
-    const double* kN;      // unscaled PH constant    [S]
+    // PH objective terms (attach_PH_to_objective, phbase.py:617-699), evaluated
+    // in registers: q_j += W_on*W - prox_on*rho*xbar, p_j = prox_on*rho,
+    // k = prox_on * sum rho/2 xbar^2, xbar = xbar_node[xbar_idx]
+    const double* W;       // [N*S]
+    const double* rho;     // [N*S]
+    const double* xbar_node;
+    const int32_t* xbar_idx;  // [N*S]
+    int32_t W_on, prox_on;
     double* xT;            // scaled x [n*S]   (generic-path hand-over)
     double* yT;            // scaled y [m*S]
     double* x;             // PDHG warm start (= xT)
@@ -116,7 +131,8 @@ struct LaneIO {
     double kkt_tol;
     double reg;
     int32_t refine;
-    int32_t as_rounds;     // active-set rounds per kernel
+    int32_t as_rounds;     // active-set rounds after the interior point (phx_lane_cold)
+    int32_t warm_rounds;   // active-set rounds per warm pass
 };
 
 // Data access for one lane: scenario-varying numbers in registers; the
@@ -128,20 +144,32 @@ struct Data {
     const int sc;
     double av[PT::NMAX_V];
     double qn[PT::NMAX_S], pn[PT::NMAX_S];
+    double kn;
 
     PHX_LD Data(const LaneIO& io_, int sc_) : io(io_), sc(sc_) {
         const int S = io.S;
         PHX_UNROLL for (int v = 0; v < PT::nvar(); ++v) av[v] = io.Av[(int64_t)v * S + sc];
+        kn = 0.0;
         PHX_UNROLL for (int t = 0; t < PT::nslot(); ++t) {
-            qn[t] = io.qN[(int64_t)t * S + sc];
-            pn[t] = io.pN[(int64_t)t * S + sc];
+            const int64_t o = (int64_t)t * S + sc;
+            double q = 0.0, p = 0.0;
+            if (io.W_on) q = io.W[o];
+            if (io.prox_on) {
+                const double r = io.rho[o], xb = io.xbar_node[io.xbar_idx[o]];
+                q -= r * xb;
+                p = r;
+                kn += 0.5 * r * xb * xb;
+            }
+            qn[t] = q;
+            pn[t] = p;
         }
     }
     PHX_LD double A(int k) const { return PT::kvar(k) < 0 ? PT::Ac(k) : av[PT::kvar(k)]; }
-    PHX_LD double dc(int j) const { return PT::dcs(j); }
-    PHX_LD double dr(int i) const { return PT::drs(i); }
-    PHX_LD double idc(int j) const { return PT::idcs(j); }   // 1/dc
-    PHX_LD double idr(int i) const { return PT::idrs(i); }   // 1/dr
+    // scaling of the problem the lane solver works on (1 when unscaled)
+    PHX_LD double dc(int j) const { return PT::scaled() ? PT::dcs(j) : 1.0; }
+    PHX_LD double dr(int i) const { return PT::scaled() ? PT::drs(i) : 1.0; }
+    PHX_LD double idc(int j) const { return PT::scaled() ? PT::idcs(j) : 1.0; }   // 1/dc
+    PHX_LD double idr(int i) const { return PT::scaled() ? PT::idrs(i) : 1.0; }   // 1/dr
     PHX_LD double c(int j) const { return PT::c_vary() ? io.c[(int64_t)j * io.S + sc] : PT::cs(j); }
     PHX_LD double q(int j) const {
         return PT::col_slot(j) >= 0 ? c(j) + dc(j) * qn[PT::col_slot(j)] : c(j);
@@ -542,16 +570,20 @@ PHX_LD double ipm_core(const Data<PT>& D, int max_it, double tol, double* x, dou
 // ---------------------------------------------------------------------------
 // Kept as per-lane bit masks in vector registers (per-lane bool arrays would
 // become 64-bit exec-style lane masks in scalar registers and spill).
+template <bool B, class T, class E> struct Cond { typedef T type; };
+template <class T, class E> struct Cond<false, T, E> { typedef E type; };
+
 template <class PT>
 struct ASet {
-    uint64_t f = 0, u = 0;   // column j: bit j
+    typedef typename Cond<(PT::NMAX_N <= 32), uint32_t, uint64_t>::type CMask;
+    CMask f = 0, u = 0;      // column j: bit j
     uint32_t r = 0, l = 0;   // row i: bit i
-    PHX_LD bool F(int j) const { return (f >> j) & 1ull; }
-    PHX_LD bool up(int j) const { return (u >> j) & 1ull; }
+    PHX_LD bool F(int j) const { return (f >> j) & 1u; }
+    PHX_LD bool up(int j) const { return (u >> j) & 1u; }
     PHX_LD bool R(int i) const { return (r >> i) & 1u; }
     PHX_LD bool lo(int i) const { return (l >> i) & 1u; }
-    PHX_LD void setF(int j, bool v) { f = v ? (f | (1ull << j)) : (f & ~(1ull << j)); }
-    PHX_LD void setUp(int j, bool v) { u = v ? (u | (1ull << j)) : (u & ~(1ull << j)); }
+    PHX_LD void setF(int j, bool v) { f = v ? (f | ((CMask)1 << j)) : (f & ~((CMask)1 << j)); }
+    PHX_LD void setUp(int j, bool v) { u = v ? (u | ((CMask)1 << j)) : (u & ~((CMask)1 << j)); }
     PHX_LD void setR(int i, bool v) { r = v ? (r | (1u << i)) : (r & ~(1u << i)); }
     PHX_LD void setLo(int i, bool v) { l = v ? (l | (1u << i)) : (l & ~(1u << i)); }
 };
@@ -662,7 +694,7 @@ PHX_LD bool kkt_solve(const Data<PT>& D, const ASet<PT>& a, double* xp, double* 
             M[PT::pair_pos(t)] += D.A(ka) * Hinv(PT::col(ka)) * D.A(kb);
     }
     if (!cholesky<PT>(M, idg)) { PHX_LANE_FAIL(10, -1); return false; }
-    PHX_UNROLL for (int it = 0; it < KKT_REFINE; ++it) {
+    PHX_REFINE_LOOP for (int it = 0; it < KKT_REFINE; ++it) {
         double r1[NN], t[MM];
         {
             double atz[NN];
@@ -707,38 +739,41 @@ PHX_LD bool kkt_solve(const Data<PT>& D, const ASet<PT>& a, double* xp, double* 
 // changed, 2 not certified and nothing to change.
 template <class PT>
 PHX_LD int certify_update(const Data<PT>& D, ASet<PT>& a, const double* xp, const double* z, double kkt_tol) {
+    typedef typename ASet<PT>::CMask CM;
     double qmax = 0.0;
     PHX_UNROLL for (int j = 0; j < PT::n(); ++j) qmax = fmax(qmax, fabs(D.q(j) * D.idc(j)));
     const double dtol = kkt_tol * (1.0 + qmax);
     const double ptol = kkt_tol;
-    bool ok = true, changed = false;
+    // branch-free: violations are gathered into bit masks, applied at the end
+    bool bad = false;                 // a violation the active set cannot fix
+    CM enter_lo = 0, enter_up = 0, leave = 0;
     double atz[PT::NMAX_N];
     D.matvec_t(z, atz);
     PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
         const double d = D.dc(j);
         const double lam = (D.q(j) + D.p(j) * xp[j] + atz[j]) * D.idc(j);
-        if (a.F(j)) {
-            bool below = false, above = false;
-            if (PT::lfin(j)) {
-                const double lo = D.l(j);
-                below = xp[j] < lo && (lo - xp[j]) * d > ptol * (1.0 + fabs(lo * d));
-            }
-            if (PT::ufin(j)) {
-                const double hi = D.u(j);
-                above = xp[j] > hi && (xp[j] - hi) * d > ptol * (1.0 + fabs(hi * d));
-            }
-            if (below) { ok = false; changed = true; a.setF(j, false); a.setUp(j, false); PHX_LANE_FAIL(1, j); }
-            else if (above) { ok = false; changed = true; a.setF(j, false); a.setUp(j, true); PHX_LANE_FAIL(2, j); }
-            else if (fabs(lam) > dtol) { ok = false; PHX_LANE_FAIL(3, j); }
-        } else if (!PT::fixed(j)) {
-            if (!a.up(j) && lam < -dtol) { ok = false; changed = true; a.setF(j, true); PHX_LANE_FAIL(4, j); }
-            if (a.up(j) && lam > dtol) { ok = false; changed = true; a.setF(j, true); a.setUp(j, false); PHX_LANE_FAIL(5, j); }
+        const bool F = a.F(j), U = a.up(j);
+        bool below = false, above = false;
+        if (PT::lfin(j)) {
+            const double lo = D.l(j);
+            below = F && xp[j] < lo && (lo - xp[j]) * d > ptol * (1.0 + fabs(lo * d));
         }
+        if (PT::ufin(j)) {
+            const double hi = D.u(j);
+            above = F && !below && xp[j] > hi && (xp[j] - hi) * d > ptol * (1.0 + fabs(hi * d));
+        }
+        bad = bad || (F && !below && !above && fabs(lam) > dtol);
+        const bool lv = !PT::fixed(j) && !F && (U ? lam > dtol : lam < -dtol);
+        enter_lo |= (CM)below << j;
+        enter_up |= (CM)above << j;
+        leave |= (CM)lv << j;
     }
+    uint32_t act_lo = 0, act_up = 0, drop = 0;
     double axp[PT::NMAX_M];
     D.matvec(xp, axp);
     PHX_UNROLL for (int i = 0; i < PT::m(); ++i) {
         const double d = D.dr(i), id = D.idr(i);
+        const bool R = a.R(i), L = a.lo(i);
         bool below = false, above = false;
         if (PT::blfin(i)) {
             const double lo = D.bl(i);
@@ -748,28 +783,27 @@ PHX_LD int certify_update(const Data<PT>& D, ASet<PT>& a, const double* xp, cons
             const double hi = D.bu(i);
             above = axp[i] > hi && (axp[i] - hi) * id > ptol * (1.0 + fabs(hi * id));
         }
-        if (!a.R(i)) {
-            if (below) { ok = false; changed = true; a.setR(i, true); a.setLo(i, true); PHX_LANE_FAIL(6, i); }
-            else if (above) { ok = false; changed = true; a.setR(i, true); a.setLo(i, false); PHX_LANE_FAIL(7, i); }
-        } else {
-            if (below || above) { ok = false; PHX_LANE_FAIL(11, i); }
-            if (!PT::eq(i)) {
-                const double yy = -z[i] * d;
-                if (a.lo(i) && yy < -dtol) { ok = false; changed = true; a.setR(i, false); PHX_LANE_FAIL(8, i); }
-                if (!a.lo(i) && yy > dtol) { ok = false; changed = true; a.setR(i, false); PHX_LANE_FAIL(9, i); }
-            }
-        }
+        bad = bad || (R && (below || above));
+        const double yy = -z[i] * d;
+        const bool dr = !PT::eq(i) && R && (L ? yy < -dtol : yy > dtol);
+        act_lo |= (uint32_t)(!R && below) << i;
+        act_up |= (uint32_t)(!R && !below && above) << i;
+        drop |= (uint32_t)dr << i;
     }
-    return ok ? 0 : (changed ? 1 : 2);
+    // primal-dual active-set update: violated bounds / rows enter, wrong-signed
+    // multipliers leave
+    a.f = (a.f & ~(enter_lo | enter_up)) | leave;
+    a.u = (a.u & ~(enter_lo | leave)) | enter_up;
+    a.r = (a.r | act_lo | act_up) & ~drop;
+    a.l = (a.l & ~act_up) | act_lo;
+    const bool changed = (enter_lo | enter_up | leave) != 0 || (act_lo | act_up | drop) != 0;
+    return changed ? 1 : (bad ? 2 : 0);
 }
 
 // KKT solve / certificate / active-set update rounds from (a, xp, z).
 template <class PT>
 PHX_LD bool as_rounds(const Data<PT>& D, ASet<PT>& a, const LaneIO& io, int rounds, double* xp, double* z) {
-#if defined(__HIPCC__) || defined(__HIPCC_RTC__)
-#pragma nounroll
-#endif
-    for (int r = 0; r < rounds; ++r) {
+    PHX_NOUNROLL for (int r = 0; r < rounds; ++r) {
         PHX_LANE_STAT(0);
         if (!kkt_solve<PT>(D, a, xp, z)) return false;
         const int c = certify_update<PT>(D, a, xp, z, io.kkt_tol);
@@ -784,7 +818,7 @@ template <class PT>
 PHX_LD void write_certified(const LaneIO& io, const Data<PT>& D, int sc, const ASet<PT>& a, const double* xp,
                             const double* z, int its) {
     const int S = io.S;
-    double f = io.kN[sc];
+    double f = D.kn;
     PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
         const double xu = xp[j] * D.dc(j);
         io.x_out[(int64_t)j * S + sc] = xu;
@@ -814,10 +848,11 @@ PHX_LD bool warm_lane(const LaneIO& io, int sc) {
     double xp[NN], z[MM];
     PHX_UNROLL for (int j = 0; j < PT::n(); ++j) xp[j] = 0.0;
     PHX_UNROLL for (int i = 0; i < PT::m(); ++i) z[i] = 0.0;
-    if (as_rounds<PT>(D, a, io, io.as_rounds, xp, z)) {
+    if (as_rounds<PT>(D, a, io, io.warm_rounds, xp, z)) {
         write_certified<PT>(io, D, sc, a, xp, z, 0);
         return false;
     }
+    aset_store<PT>(io, sc, a);   // the updated active set seeds the next pass
     io.status[sc] = 0;
     io.flags[sc] = 0;
     return true;
@@ -843,14 +878,17 @@ PHX_LD bool cold_lane(const LaneIO& io, int sc) {
             return false;
         }
     }
-    // hand the IPM point to the generic PDHG path
+    // hand the IPM point to the generic PDHG path (which works scaled:
+    // x_s = x / dc, y_s = y / dr)
     PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
         const int64_t o = (int64_t)j * S + sc;
-        io.xT[o] = x[j]; io.x[o] = x[j]; io.x0[o] = x[j];
+        const double v = PT::scaled() ? x[j] : x[j] * PT::idcs(j);
+        io.xT[o] = v; io.x[o] = v; io.x0[o] = v;
     }
     PHX_UNROLL for (int i = 0; i < PT::m(); ++i) {
         const int64_t o = (int64_t)i * S + sc;
-        io.yT[o] = y[i]; io.y[o] = y[i]; io.y0[o] = y[i];
+        const double v = PT::scaled() ? y[i] : y[i] * PT::idrs(i);
+        io.yT[o] = v; io.y[o] = v; io.y0[o] = v;
     }
     io.err[sc] = err;
     io.iters[sc] = its;

@@ -13,7 +13,7 @@ passes solver options (``iter0_solver_options`` / ``iterk_solver_options``,
 phbase.py:273-275): keys ``pdhg_max_iters``, ``pdhg_check_every``,
 ``pdhg_restart_max``, ``polish``, ``polish_refine``, ``polish_below``,
 ``kkt_tol``, ``opt_tol``, ``polish_reg``, ``warm_start``, ``ipm_after``,
-``ipm_max_it``, ``ipm_tol``, ``lane_solver``, ``as_rounds``.
+``ipm_max_it``, ``ipm_tol``, ``lane_solver``, ``as_rounds``, ``warm_passes``.
 """
 import ctypes
 import inspect
@@ -41,6 +41,7 @@ SOLVER_DEFAULTS = {
     "ipm_tol": 1e-10,
     "lane_solver": 1,
     "as_rounds": 4,
+    "warm_passes": 1,
 }
 
 OPTIMAL, ITER_LIMIT, NUMERIC_FAIL = 1, 2, 3
@@ -98,6 +99,7 @@ class SPOpt(SPBase):
         so.ipm_tol = float(o["ipm_tol"])
         so.lane_solver = int(o["lane_solver"])
         so.as_rounds = int(o["as_rounds"])
+        so.warm_passes = int(o["warm_passes"])
         return so
 
     def _set_ph_terms(self):
@@ -135,7 +137,8 @@ class SPOpt(SPBase):
         n_bad = int(stt.not_optimal)
         self.solve_stats.append({"pdhg_iters": int(total.value), "pdhg_ms": stt.pdhg_ms, "launches": stt.pdhg_launches,
                                  "lane_iters": stt.lane_iters, "polish_ms": stt.polish_ms, "ipm_ms": stt.ipm_ms,
-                                 "lane_ms": stt.lane_ms, "lane_warm_ms": stt.lane_warm_ms, "lane_certified": stt.lane_certified,
+                                 "lane_ms": stt.lane_ms, "lane_warm_ms": stt.lane_warm_ms,
+                                 "lane_warm_list_ms": stt.lane_warm_list_ms, "lane_certified": stt.lane_certified,
                                  "lane_warm_certified": stt.lane_warm_certified,
                                  "wall_s": time.perf_counter() - t0, "not_optimal": n_bad})
         if n_bad and gripe:
