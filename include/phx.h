@@ -89,6 +89,11 @@ typedef struct phx_solve_opts {
                                  as_rounds rounds in-kernel; k > 1: k passes of
                                  one round each, passes 2..k over the
                                  compacted lanes whose active set changed    */
+    int32_t defer;            /* 1: with the lane solver, phx_solve returns
+                                 right after enqueueing the lane kernels (no
+                                 host synchronisation); phx_solve_finish then
+                                 completes the solve (generic path for the
+                                 lanes the lane solver could not certify)     */
 } phx_solve_opts;
 
 /* Statistics of the most recent phx_solve (HIP events on the solve stream). */
@@ -106,6 +111,8 @@ typedef struct phx_solve_stats {
     int32_t lane_certified;   /* scenarios certified by the lane solver       */
     int32_t lane_warm_certified; /* ... of which by the warm active-set pass  */
     int32_t not_optimal;      /* scenarios without an optimal status          */
+    int32_t stragglers;       /* lanes the lane solver handed to the generic
+                                 path (their x was final only after it)       */
     int32_t jit;              /* 1 if this context has a specialised kernel   */
 } phx_solve_stats;
 
@@ -144,6 +151,15 @@ const char* phx_build_info(void);
  * polish workspace.  Synchronises the device (setup only).                 */
 int phx_set_problem(phx_ctx* ctx, const phx_problem_desc* desc);
 
+/* Per-scenario column bounds ([n][S], unscaled, device) replacing the
+ * problem's own for the following solves — how the engine fixes nonants
+ * (lb = ub = value: SPOpt._fix_nonants / _restore_nonants, spopt.py:557-662;
+ * Xhat_Eval, utils/xhat_eval.py:293-322).  lb = ub = NULL restores the
+ * problem's bounds.  While overridden, solves use the generic path (the lane
+ * kernels are specialised on the original bound structure).  Enqueued on
+ * `stream`; the arrays may be released after the call's work has run.      */
+int phx_set_bounds(phx_ctx* ctx, const double* lb, const double* ub, void* stream);
+
 /* PH objective terms for the next solve (attach_PH_to_objective,
  * phbase.py:617-699; W_on/prox_on toggles :409-440):
  *   qN[j][s] = W_on*W[j][s] - prox_on*rho[j][s]*xbar(s,j)
@@ -168,6 +184,14 @@ int phx_solve(phx_ctx* ctx, const phx_solve_opts* opts,
               int32_t* status_out, int32_t* iters_out,
               int32_t* total_iters_host, void* stream);
 
+/* Completes a solve started with opts.defer = 1: waits for the lane kernels
+ * (host synchronisation), runs the generic path on the lanes they left, and
+ * reports how many there were (*stragglers_host; 0 = every lane's outputs
+ * were already final when phx_solve returned).  No-op if nothing is pending.
+ * Outputs land in the arrays given to phx_solve.  Replaces the tail of
+ * SPOpt.solve_loop (spopt.py:284-307: statuses, feasibility, timing).       */
+int phx_solve_finish(phx_ctx* ctx, int32_t* stragglers_host, int32_t* total_iters_host);
+
 /* Objective of the caller's point x ([n][S], unscaled) under the PH terms last
  * set by phx_set_ph_terms: obj[s] = c'x + qN'x_N + 0.5 pN x_N^2 + kN — what
  * the reference evaluates as pyo.value(objective) in Eobjective
@@ -183,7 +207,8 @@ int phx_xbar(phx_ctx* ctx, const phx_tree_desc* tree, const double* x,
              void* stream);
 
 /* Update_W + convergence_diff local part (phbase.py:293-343):
- *   W[j][s] += rho[j][s]*(x_N - xbar)   (if update_w)
+ *   W[j][s] = W_in[j][s] + rho[j][s]*(x_N - xbar)   (if update_w; W_in may
+ *             equal W — in place — or be the other buffer of a pair)
  *   dsum[s]  = sum_j |x_N - xbar|            (dsum may be NULL when the
  *                                             segments cover every scenario)
  * then seg_sums[r] = sum of dsum over local scenarios [seg_s0[r], seg_s1[r])
@@ -191,7 +216,7 @@ int phx_xbar(phx_ctx* ctx, const phx_tree_desc* tree, const double* x,
  * segments partition the local scenarios, W, dsum and the segment partials
  * come out of one fused pass (k_update_w_seg).                              */
 int phx_update_w(phx_ctx* ctx, const double* x, const double* xbar_node,
-                 const int32_t* xbar_idx, const double* rho, double* W,
+                 const int32_t* xbar_idx, const double* rho, const double* W_in, double* W,
                  int32_t update_w, double* dsum, int32_t nseg,
                  const int32_t* seg_s0_host, const int32_t* seg_s1_host,
                  double* seg_sums, void* stream);

@@ -40,6 +40,7 @@ class SolveOpts(ctypes.Structure):
         ("reg", c_double),
         ("ipm_after", c_int32), ("ipm_max_it", c_int32), ("ipm_tol", c_double),
         ("lane_solver", c_int32), ("as_rounds", c_int32), ("warm_passes", c_int32),
+        ("defer", c_int32),
     ]
 
 
@@ -48,7 +49,7 @@ class SolveStats(ctypes.Structure):
         ("pdhg_ms", c_double), ("polish_ms", c_double), ("ipm_ms", c_double), ("lane_ms", c_double),
         ("lane_warm_ms", c_double), ("lane_warm_list_ms", c_double),
         ("lane_iters", c_double), ("pdhg_launches", c_int32), ("total_iters", c_int32),
-        ("lane_certified", c_int32), ("lane_warm_certified", c_int32), ("not_optimal", c_int32), ("jit", c_int32),
+        ("lane_certified", c_int32), ("lane_warm_certified", c_int32), ("not_optimal", c_int32), ("stragglers", c_int32), ("jit", c_int32),
     ]
 
 
@@ -65,8 +66,8 @@ class TreeDesc(ctypes.Structure):
 
 # every symbol of include/phx.h (tests check the library exports all of them)
 SYMBOLS = [
-    "create", "destroy", "last_error", "build_info", "set_problem", "set_ph_terms",
-    "solve", "objective", "xbar", "update_w", "expect", "export_slots", "last_solve_stats", "jit_info",
+    "create", "destroy", "last_error", "build_info", "set_problem", "set_bounds", "set_ph_terms",
+    "solve", "solve_finish", "objective", "xbar", "update_w", "expect", "export_slots", "last_solve_stats", "jit_info",
 ]
 
 
@@ -98,16 +99,18 @@ class Lib:
         self.last_error = fn("last_error", ctypes.c_char_p, [c_void_p])
         self.build_info = fn("build_info", ctypes.c_char_p, [])
         self.set_problem = fn("set_problem", ctypes.c_int, [c_void_p, ctypes.POINTER(ProblemDesc)])
+        self.set_bounds = fn("set_bounds", ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p])
         self.set_ph_terms = fn("set_ph_terms", ctypes.c_int,
                                [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p])
         self.solve = fn("solve", ctypes.c_int,
                         [c_void_p, ctypes.POINTER(SolveOpts), c_void_p, c_void_p, c_void_p, c_void_p,
                          c_void_p, P_i32, c_void_p])
+        self.solve_finish = fn("solve_finish", ctypes.c_int, [c_void_p, P_i32, P_i32])
         self.objective = fn("objective", ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p])
         self.xbar = fn("xbar", ctypes.c_int,
                        [c_void_p, ctypes.POINTER(TreeDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p])
         self.update_w = fn("update_w", ctypes.c_int,
-                           [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,
+                           [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,
                             c_int32, P_i32, P_i32, c_void_p, c_void_p])
         self.expect = fn("expect", ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p])
         self.export_slots = fn("export_slots", ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p])

@@ -126,6 +126,7 @@ struct LaneIO {
     int32_t* iters_out;    // [S] caller's iteration counts
     int32_t* lanes_out;    // compacted uncertified lanes
     int32_t* count_out;    // their number (atomic)
+    int32_t* counts_next;  // [16] zeroed by block 0 (the next solve's counters), or null
     int32_t max_it;
     double ipm_tol;
     double kkt_tol;
@@ -900,6 +901,11 @@ PHX_LD bool cold_lane(const LaneIO& io, int sc) {
 // Compact the lanes that still need work into out[0..*count): one atomic per
 // wavefront, lane order kept within the wavefront.  Every lane of the
 // wavefront must reach this call.
+// Zero the next solve's counters (double-buffered, so no memset launch).
+__device__ __forceinline__ void zero_next_counts(int32_t* next) {
+    if (next && blockIdx.x == 0 && threadIdx.x < 16) next[threadIdx.x] = 0;
+}
+
 __device__ __forceinline__ void compact_lane(bool still, int sc, int32_t* out, int32_t* count) {
     const unsigned long long b = __ballot(still);
     const int lane = threadIdx.x & 63;

@@ -63,6 +63,11 @@ class PHBase(SPOpt):
         """W = 0, rho = defaultPHrho, W_on = prox_on = 0 (phbase.py:585-602)."""
         N, S = self.batch.nonant.N, self._S
         self._W = torch.zeros(max(N, 1) * S, dtype=torch.float64, device=self.device)
+        # second W buffer: an Update_W issued while a deferred solve may still
+        # owe some scenarios (stragglers) writes here and is committed by
+        # convergence_diff once the solve is known final (see _settle)
+        self._W_alt = torch.zeros_like(self._W)
+        self._w_uncommitted = False
         self._rho = torch.full((max(N, 1) * S,), float(self.options["defaultPHrho"]),
                                dtype=torch.float64, device=self.device)
         self.W_on = 0
@@ -107,14 +112,36 @@ class PHBase(SPOpt):
 
     def _update_w_and_diff(self, update):
         lib = self._native
+        W_out = self._W
+        if update and self._solve_pending:
+            W_out = self._W_alt                  # out of place until the solve is known final
+            self._w_uncommitted = True
         lib.check(self._ctx, lib.update_w(self._ctx, self._x.data_ptr(), self._xbar_node.data_ptr(),
                                           self._xbar_idx_t.data_ptr(), self._rho.data_ptr(),
-                                          self._W.data_ptr(), int(update), None,
+                                          self._W.data_ptr(), W_out.data_ptr(), int(update), None,
                                           self._conv_R, self._seg_s0, self._seg_s1,
                                           self._seg_sums.data_ptr(), self._stream()), "update_w")
         self._conv_cache = self._seg_sums      # consumed (all-reduced) by convergence_diff
         self._conv_value = None
+        self._conv_updated_w = bool(update)
         self._bump()
+
+    def _settle_pending(self):
+        """Finish a deferred solve; an optimistic Update_W issued behind it is
+        committed, or redone in place if some scenario's x changed (collective
+        over ranks when such an update is outstanding)."""
+        n = self._sync_solve()
+        if self._w_uncommitted:
+            if self.n_proc > 1:
+                t = torch.tensor([float(n)], dtype=torch.float64, device=self.device)
+                self.mpicomm.allreduce_(t)
+                n = int(t.item())
+            self._w_uncommitted = False
+            if n > 0:
+                self.Compute_Xbar(False)
+                self._update_w_and_diff(self._conv_updated_w)
+            else:
+                self._W, self._W_alt = self._W_alt, self._W
 
     def Update_W(self, verbose):
         """W += rho (x - xbar) (phbase.py:293-318)."""
@@ -127,19 +154,61 @@ class PHBase(SPOpt):
         if getattr(self, "_conv_cache", None) is None:
             self._update_w_and_diff(False)
         if getattr(self, "_conv_value", None) is None:
+            R = self._conv_R
             t = self._conv_cache
-            self.mpicomm.allreduce_(t)
-            v = t.cpu().numpy()
+            pending = self._solve_pending
+            redo = False
+            single = self.n_proc == 1 and self.device.type == "cuda"
+            if single:
+                # read the sums back asynchronously into pinned memory; the wait
+                # below covers it (one host synchronisation per PH step)
+                if getattr(self, "_conv_host", None) is None:
+                    self._conv_host = torch.empty(R + 1, dtype=torch.float64, pin_memory=True)
+                    self._conv_evt = torch.cuda.Event()
+                self._conv_host.copy_(t, non_blocking=True)
+                self._conv_evt.record()
+            if pending:
+                # Deferred solve: Compute_Xbar / Update_W were enqueued behind it
+                # optimistically.  Finish it now (the GPU is busy with them) and
+                # count, over all ranks, the scenarios it had to hand to the
+                # generic path: their x was not final when x-bar was formed.
+                n_local = self._sync_solve()
+                if self.n_proc > 1:
+                    t[R].fill_(float(n_local))
+                else:
+                    redo = n_local > 0
+            if single and not redo:
+                self._conv_evt.synchronize()
+                v = self._conv_host.numpy()
+            else:
+                self.mpicomm.allreduce_(t)
+                v = t.cpu().numpy()
+            if pending and (redo or (self.n_proc > 1 and v[R] > 0)):
+                # redo the step on the now final x; W from the committed buffer,
+                # updated in place (the optimistic W_alt is discarded)
+                self._w_uncommitted = False
+                upd = self._conv_updated_w
+                self.Compute_Xbar(False)
+                self._update_w_and_diff(upd)
+                t = self._conv_cache
+                if self.n_proc > 1:
+                    t[R].fill_(0.0)
+                self.mpicomm.allreduce_(t)
+                v = t.cpu().numpy()
+            if self._w_uncommitted:
+                self._W, self._W_alt = self._W_alt, self._W
+                self._w_uncommitted = False
             cnt = self._conv_counts
             tot = 0.0
-            for r in range(self._conv_R):
+            for r in range(R):
                 if cnt[r] > 0:
                     tot += v[r] / cnt[r]
-            self._conv_value = tot / self._conv_R
+            self._conv_value = tot / R
         return self._conv_value
 
     def _populate_W_cache(self, cache, padding):
         """Flat scenario-major W export (phbase.py:346-366)."""
+        self._settle()
         N, S = self.batch.nonant.N, self._S
         if len(cache) - padding < N * S:
             raise RuntimeError("W cache length mismatch detected by %s that has total W len %d but "
@@ -151,6 +220,7 @@ class PHBase(SPOpt):
 
     def W_from_flat_list(self, flat_list):
         """Set W from a flat scenario-major list (phbase.py:369-385)."""
+        self._settle()
         N, S = self.batch.nonant.N, self._S
         a = torch.as_tensor(np.asarray(flat_list[:N * S], dtype=np.float64)).view(S, N).t().contiguous()
         self._W.copy_(a.view(-1).to(self.device))
@@ -338,6 +408,7 @@ class PHBase(SPOpt):
             if self.options["display_convergence_detail"]:
                 self.report_var_values_at_rank0(header="Convergence detail:")
         else:
+            self._settle()
             self.mpicomm.Barrier()
             if self.cylinder_rank == 0 and (dprogress or verbose):
                 _global_toc("Reached user-specified limit=%d on number of PH iterations" % max_iterations)
@@ -348,6 +419,7 @@ class PHBase(SPOpt):
         have_extensions = extensions is not None
         dprogress = self.options["display_progress"]
         dtiming = self.options["display_timing"]
+        self._settle()
         self.mpicomm.Barrier()
         if self.scenario_denouement is not None:
             for sname, s in self.local_scenarios.items():

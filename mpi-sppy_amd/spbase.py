@@ -313,7 +313,9 @@ class SPBase:
         self._xbar_node = self._node_buf[:NNS1]
         self._xsqbar_node = self._node_buf[NNS1:2 * NNS1]
         self._dsum = torch.zeros(S, dtype=f64, device=self.device)
-        self._seg_sums = torch.zeros(self._conv_R, dtype=f64, device=self.device)
+        # per-emulated-rank |x - xbar| sums + one slot for the straggler count of
+        # a deferred solve (all-reduced together, phbase.convergence_diff)
+        self._seg_sums = torch.zeros(self._conv_R + 1, dtype=f64, device=self.device)
         self._expect_buf = torch.zeros(3, dtype=f64, device=self.device)
         # tree descriptor
         tiles = self._tiles
@@ -365,6 +367,8 @@ class SPBase:
 
     def _host(self, key):
         """numpy copy of a device array (cached until the next device op)."""
+        if hasattr(self, "_settle"):
+            self._settle()
         if key not in self._host_cache:
             S = self._S
             if key == "x":
@@ -391,6 +395,8 @@ class SPBase:
     def _host_write(self, key, j, s, value):
         """write-through to the device array (W / rho mirrors)."""
         S = self._S
+        if hasattr(self, "_settle"):
+            self._settle()
         t = {"W": self._W, "rho": self._rho}[key]
         t[j * S + s] = float(value)
         if key in self._host_cache:

@@ -70,6 +70,7 @@ class SPOpt(SPBase):
         self.W_on = 0
         self.prox_on = 0
         self.solve_stats = []
+        self._solve_pending = False
         if self.extensions is not None:
             if self.extension_kwargs is None:
                 self.extobject = self.extensions(self)
@@ -121,8 +122,17 @@ class SPOpt(SPBase):
             if _overrides(self.extobject, "pre_solve"):
                 for s in self.local_subproblems.values():
                     self.extobject.pre_solve(s)
+        self._settle()
         lib = self._native
         so = self._solve_opts(solver_options)
+        # Without extensions nothing reads per-scenario results right after the
+        # solve, so it is deferred: phx_solve returns once the lane kernels are
+        # enqueued and the next PH step's reductions queue behind them; every
+        # reader of solve results calls _settle() (convergence_diff finishes it
+        # and redoes the step in the rare case a scenario needed the generic path).
+        defer = (self.extensions is None and not dtiming and so.lane_solver
+                 and bool((solver_options or {}).get("defer", 1)))
+        so.defer = 1 if defer else 0
         self._set_ph_terms()
         total = ctypes.c_int32(0)
         t0 = time.perf_counter()
@@ -131,25 +141,12 @@ class SPOpt(SPBase):
                                        ctypes.byref(total), self._stream()), "solve")
         self._conv_cache = None
         self._bump()
-        stt = _native.SolveStats()
-        lib.check(self._ctx, lib.last_solve_stats(self._ctx, ctypes.byref(stt)), "last_solve_stats")
-        st = self._status
-        n_bad = int(stt.not_optimal)
-        self.solve_stats.append({"pdhg_iters": int(total.value), "pdhg_ms": stt.pdhg_ms, "launches": stt.pdhg_launches,
-                                 "lane_iters": stt.lane_iters, "polish_ms": stt.polish_ms, "ipm_ms": stt.ipm_ms,
-                                 "lane_ms": stt.lane_ms, "lane_warm_ms": stt.lane_warm_ms,
-                                 "lane_warm_list_ms": stt.lane_warm_list_ms, "lane_certified": stt.lane_certified,
-                                 "lane_warm_certified": stt.lane_warm_certified,
-                                 "wall_s": time.perf_counter() - t0, "not_optimal": n_bad})
-        if n_bad and gripe:
-            stc = st.cpu().numpy()
-            name = self.__class__.__name__
-            if self.spcomm:
-                name = self.spcomm.__class__.__name__
-            for k in np.nonzero(stc != OPTIMAL)[0][:10]:
-                print("[%s] Solve failed for scenario %s" % (name, self.local_scenario_names[k]))
-                print("status=", {ITER_LIMIT: "iteration limit", NUMERIC_FAIL: "numerical failure"}.get(
-                    int(stc[k]), int(stc[k])))
+        rec = {"wall_s": None, "t0": t0, "gripe": gripe}
+        self.solve_stats.append(rec)
+        if total.value == -1:
+            self._solve_pending = True
+        else:
+            self._record_solve(rec, int(total.value), 0)
         if self.extensions is not None:
             if _overrides(self.extobject, "post_solve"):
                 for s in self.local_subproblems.values():
@@ -161,8 +158,55 @@ class SPOpt(SPBase):
                 print("Batched solve times (seconds): min=%4.2f mean=%4.2f max=%4.2f"
                       % (min(allt), sum(allt) / len(allt), max(allt)))
 
+    def _record_solve(self, rec, total, stragglers):
+        lib = self._native
+        stt = _native.SolveStats()
+        lib.check(self._ctx, lib.last_solve_stats(self._ctx, ctypes.byref(stt)), "last_solve_stats")
+        n_bad = int(stt.not_optimal)
+        t0, gripe = rec.pop("t0"), rec.pop("gripe")
+        rec.update({"pdhg_iters": total, "pdhg_ms": stt.pdhg_ms, "launches": stt.pdhg_launches,
+                    "lane_iters": stt.lane_iters, "polish_ms": stt.polish_ms, "ipm_ms": stt.ipm_ms,
+                    "lane_ms": stt.lane_ms, "lane_warm_ms": stt.lane_warm_ms,
+                    "lane_warm_list_ms": stt.lane_warm_list_ms, "lane_certified": stt.lane_certified,
+                    "lane_warm_certified": stt.lane_warm_certified, "stragglers": stragglers,
+                    "wall_s": time.perf_counter() - t0, "not_optimal": n_bad})
+        if n_bad and gripe:
+            stc = self._status.cpu().numpy()
+            name = self.__class__.__name__
+            if self.spcomm:
+                name = self.spcomm.__class__.__name__
+            for k in np.nonzero(stc != OPTIMAL)[0][:10]:
+                print("[%s] Solve failed for scenario %s" % (name, self.local_scenario_names[k]))
+                print("status=", {ITER_LIMIT: "iteration limit", NUMERIC_FAIL: "numerical failure"}.get(
+                    int(stc[k]), int(stc[k])))
+
+    def _sync_solve(self):
+        """Finish a deferred solve (phx_solve_finish); returns the number of local
+        scenarios that needed the generic path (their x changed)."""
+        if not self._solve_pending:
+            return 0
+        lib = self._native
+        strag = ctypes.c_int32(0)
+        total = ctypes.c_int32(0)
+        lib.check(self._ctx, lib.solve_finish(self._ctx, ctypes.byref(strag), ctypes.byref(total)),
+                  "solve_finish")
+        self._solve_pending = False
+        self._record_solve(self.solve_stats[-1], int(total.value), int(strag.value))
+        if strag.value:
+            self._bump()
+        return int(strag.value)
+
+    def _settle(self):
+        """Make solve results and W final before anything reads them."""
+        if self._solve_pending or getattr(self, "_w_uncommitted", False):
+            self._settle_pending()
+
+    def _settle_pending(self):
+        self._sync_solve()
+
     # ------------------------------------------------------------ expectations
     def _expect(self, values):
+        self._settle()
         lib = self._native
         lib.check(self._ctx, lib.expect(self._ctx, self._prob.data_ptr(), values.data_ptr(),
                                         self._status.data_ptr(), self._expect_buf.data_ptr(),
@@ -179,6 +223,7 @@ class SPOpt(SPBase):
 
     def _objective_now(self):
         """Objective of the current x under the current W/xbar/rho and W_on/prox_on."""
+        self._settle()
         if not hasattr(self, "_obj_eval"):
             self._obj_eval = torch.zeros_like(self._obj)
         self._set_ph_terms()

@@ -136,3 +136,24 @@ def test_convthresh_stops_before_solve(emu):
     it = o.iterk(500, 1e-4) if o.iter0() is not None else None
     assert ph._PHIter == it
     assert conv < 1e-4
+
+
+@pytest.mark.parametrize("so", [{"as_rounds": 0, "ipm_max_it": 2}, {"as_rounds": 1, "ipm_max_it": 3}])
+def test_deferred_solve_with_stragglers_matches_sync(emu, so):
+    """Deferred solves (phx_solve opts.defer) let Compute_Xbar/Update_W run
+    behind the solve; when scenarios must go to the generic path (forced here by
+    starving the interior point), convergence_diff finishes the solve and redoes
+    the step.  The trajectory must equal the synchronous one."""
+    S = 24
+    runs = []
+    for defer in (1, 0):
+        o = dict(so, defer=defer)
+        ph, conv, Eobj, tb = run_engine(farmer.scenario_creator, farmer.scenario_names_creator(S),
+                                        {"num_scens": S}, 4, lib=emu, device="cpu",
+                                        options={"iter0_solver_options": o, "iterk_solver_options": o})
+        runs.append((ph, conv, Eobj, tb))
+    (a, ca, Ea, ta), (b, cb, Eb, tb_) = runs
+    assert any(s.get("stragglers", 0) > 0 for s in a.solve_stats)
+    assert np.array_equal(a.W_array(), b.W_array())
+    assert np.array_equal(a.xbar_by_node()["ROOT"][0], b.xbar_by_node()["ROOT"][0])
+    assert ca == cb and Ea == Eb and ta == tb_

@@ -96,3 +96,22 @@ def test_farmer_100k_sampled_oracle(gpu_lib):
     assert rel(o.xn(), xn[sample]) < 1e-6
     assert rel(o.obj, obj[sample]) < 1e-8
     assert 0.0 < conv < 1e4 and np.isfinite(Eobj) and np.isfinite(tb)
+
+
+def test_deferred_solve_with_stragglers_matches_sync(gpu_lib):
+    """Deferred solve + optimistic Compute_Xbar/Update_W; stragglers forced by
+    starving the interior point: the redo path must reproduce the synchronous run."""
+    S = 300
+    so = {"as_rounds": 0, "ipm_max_it": 2}
+    runs = []
+    for defer in (1, 0):
+        o = dict(so, defer=defer)
+        ph, conv, Eobj, tb = run_engine(farmer.scenario_creator, farmer.scenario_names_creator(S),
+                                        {"num_scens": S}, 4, lib=gpu_lib,
+                                        options={"iter0_solver_options": o, "iterk_solver_options": o})
+        assert all(s["not_optimal"] == 0 for s in ph.solve_stats)
+        runs.append((ph, conv, Eobj, tb))
+    (a, ca, Ea, ta), (b, cb, Eb, tb_) = runs
+    assert any(s.get("stragglers", 0) > 0 for s in a.solve_stats)
+    assert rel(a.W_array(), b.W_array()) < 1e-12
+    assert rel(ca, cb) < 1e-12 and rel(Ea, Eb) < 1e-12 and rel(ta, tb_) < 1e-12
