@@ -25,7 +25,6 @@ import torch
 
 from . import _native
 from .spopt import SPOpt
-from .views import ScenarioView
 from .spbase import _global_toc
 
 
@@ -51,7 +50,6 @@ class PHBase(SPOpt):
         self.conv = None
         self._PHIter = 0
         self.attach_xbars()
-        self._make_views()
 
     # ------------------------------------------------------------ state
     def attach_xbars(self):
@@ -84,10 +82,6 @@ class PHBase(SPOpt):
     def PH_Prep(self, attach_duals=True, attach_prox=True):
         self.attach_Ws_and_prox()
         self.attach_PH_to_objective(attach_duals, attach_prox)
-
-    def _make_views(self):
-        self.local_scenarios = {nm: ScenarioView(self, k, nm) for k, nm in enumerate(self.local_scenario_names)}
-        self.local_subproblems = self.local_scenarios
 
     def options_check(self):
         required = ["solver_name", "PHIterLimit", "defaultPHrho", "convthresh", "verbose", "display_progress"]
@@ -277,6 +271,8 @@ class PHBase(SPOpt):
         if self.W_disabled:
             self._reenable_W()
         self._disable_prox()
+        # fixed variables can lead to an invalid lower bound
+        self._restore_original_fixedness()
         self.solve_loop(solver_options=solver_options, dis_prox=False, gripe=True, tee=False, verbose=verbose)
         bound = self.Ebound(verbose)
         self._reenable_prox()

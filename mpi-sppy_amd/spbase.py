@@ -397,10 +397,12 @@ class SPBase:
         S = self._S
         if hasattr(self, "_settle"):
             self._settle()
-        t = {"W": self._W, "rho": self._rho}[key]
+        t = self._x if key == "x" else {"W": self._W, "rho": self._rho}[key]
         t[j * S + s] = float(value)
         if key in self._host_cache:
             self._host_cache[key][j, s] = float(value)
+        if key == "x":
+            self._conv_cache = None
 
     @property
     def spcomm(self):

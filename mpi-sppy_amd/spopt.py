@@ -24,6 +24,7 @@ import torch
 
 from . import _native
 from .spbase import SPBase
+from .views import ScenarioView
 
 SOLVER_DEFAULTS = {
     "pdhg_max_iters": 200000,
@@ -71,11 +72,16 @@ class SPOpt(SPBase):
         self.prox_on = 0
         self.solve_stats = []
         self._solve_pending = False
+        self._make_views()
         if self.extensions is not None:
             if self.extension_kwargs is None:
                 self.extobject = self.extensions(self)
             else:
                 self.extobject = self.extensions(self, **self.extension_kwargs)
+
+    def _make_views(self):
+        self.local_scenarios = {nm: ScenarioView(self, k, nm) for k, nm in enumerate(self.local_scenario_names)}
+        self.local_subproblems = self.local_scenarios
 
     # ------------------------------------------------------------ solve
     def _solve_opts(self, solver_options):
@@ -123,6 +129,7 @@ class SPOpt(SPBase):
                 for s in self.local_subproblems.values():
                     self.extobject.pre_solve(s)
         self._settle()
+        self._apply_fixing()
         lib = self._native
         so = self._solve_opts(solver_options)
         # Without extensions nothing reads per-scenario results right after the
@@ -141,6 +148,10 @@ class SPOpt(SPBase):
                                        ctypes.byref(total), self._stream()), "solve")
         self._conv_cache = None
         self._bump()
+        if getattr(self, "_fix_lb", None) is not None:
+            # fixed columns come back through the solver's column scaling; give
+            # them their exact values (a fixed Var's value is the fixed value)
+            self._set_nonant_x(self._fix_val, self._fixed)
         rec = {"wall_s": None, "t0": t0, "gripe": gripe}
         self.solve_stats.append(rec)
         if total.value == -1:
@@ -269,3 +280,178 @@ class SPOpt(SPBase):
     def _create_solvers(self, presolve=True):
         """The native context built in SPBase already holds the batched 'solver'."""
         return None
+
+    # ------------------------------------------------------------ nonant fixing
+    # spopt.py:536-742.  A fixed nonant is a column with lb = ub = value (what a
+    # persistent solver's update_var does); fixedness and values live on the
+    # host as [S_local][N] arrays (the reference's per-scenario caches, same
+    # slot order), and the solve sees them through phx_set_bounds, uploaded
+    # only when fixedness changed.  Nothing is fixed originally (creators
+    # express fixed data as bounds).
+    def _fix_arrays(self):
+        if getattr(self, "_fixed", None) is None:
+            S, N = self._S, self.batch.nonant.N
+            self._fixed = np.zeros((S, N), dtype=bool)
+            self._fix_val = np.zeros((S, N))
+            self._fix_dirty = False
+        return self._fixed, self._fix_val
+
+    def _nonant_x(self):
+        """(S_local, N) current nonant values (host copy)."""
+        return self.nonant_values()
+
+    def _set_nonant_x(self, vals, mask=None):
+        """Write nonant values (S_local, N) into x on the device (where mask)."""
+        self._settle()
+        nn = self.batch.nonant
+        S = self._S
+        cols = torch.as_tensor(nn.slot_col.astype(np.int64), device=self.device)
+        xv = self._x.view(-1, S)
+        new = torch.as_tensor(np.ascontiguousarray(np.asarray(vals, dtype=np.float64).T), device=self.device)
+        if mask is not None:
+            m = torch.as_tensor(np.ascontiguousarray(np.asarray(mask, dtype=bool).T), device=self.device)
+            new = torch.where(m, new, xv[cols])
+        xv[cols] = new
+        self._bump()
+
+    def _cache_by_slot(self, cache, stage_max=None, root_only=False):
+        """Per (scenario, slot) values from an ndn-keyed cache, with the
+        reference's errors (spopt.py:569-583); returns (vals, mask)."""
+        nn = self.batch.nonant
+        S, N = self._S, nn.N
+        vals = np.zeros((S, N))
+        mask = np.zeros((S, N), dtype=bool)
+        nlen_of = {}
+        for t in range(nn.nstages):
+            nlen_of[t] = nn.nlen(t)
+        for t in range(nn.nstages):
+            if root_only and t > 0:
+                break
+            if stage_max is not None and t + 1 > stage_max:
+                break
+            slots = np.nonzero(nn.slot_stage == t + 1)[0]
+            names = nn.node_names[t] if not root_only else None
+            groups = {"ROOT": np.arange(S)} if names is None else {}
+            if names is not None:
+                arr = np.asarray(names)
+                for nd in dict.fromkeys(names):
+                    groups[nd] = np.nonzero(arr == nd)[0]
+            for nd, ss in groups.items():
+                if root_only:
+                    c = cache
+                    if c is None:
+                        raise RuntimeError("Empty root cache for scen={}".format(self.local_scenario_names[0]))
+                    if len(c) != nlen_of[0]:
+                        raise RuntimeError("Needed {} nonant Vars for 'ROOT', got {}".format(nlen_of[0], len(c)))
+                else:
+                    if nd not in cache:
+                        raise RuntimeError("Could not find {} in {}".format(nd, cache))
+                    c = cache[nd]
+                    if c is None:
+                        raise RuntimeError("Empty cache for scen={}, node={}"
+                                           .format(self.local_scenario_names[int(ss[0])], nd))
+                    if len(c) != nlen_of[t]:
+                        raise RuntimeError("Needed {} nonant Vars for {}, got {}".format(nlen_of[t], nd, len(c)))
+                c = np.asarray(c, dtype=np.float64)
+                for j in slots:
+                    vals[ss, j] = c[nn.slot_local[j]]
+                    mask[ss, j] = True
+        return vals, mask
+
+    def _fix_where(self, vals, mask):
+        fixed, fv = self._fix_arrays()
+        fixed |= mask
+        fv[mask] = vals[mask]
+        self._fix_dirty = True
+        self._set_nonant_x(vals, mask)
+
+    def _fix_nonants(self, cache):
+        """Fix every local scenario's nonants at ``cache[ndn][i]`` (spopt.py:557-591)."""
+        vals, mask = self._cache_by_slot(cache)
+        self._fix_where(vals, mask)
+
+    def _fix_root_nonants(self, root_cache):
+        """Fix the ROOT nonants at ``root_cache[i]`` (spopt.py:593-636)."""
+        if "ROOT" not in self.all_nodenames:
+            raise RuntimeError("Could not find a 'ROOT' node in scen {}".format(self.local_scenario_names[0]))
+        vals, mask = self._cache_by_slot(root_cache, root_only=True)
+        self._fix_where(vals, mask)
+
+    def _save_nonants(self):
+        """nonant_cache / fixedness_cache <- current values and fixedness (spopt.py:665-687)."""
+        fixed, _ = self._fix_arrays()
+        self.nonant_cache = np.ascontiguousarray(self._nonant_x())
+        self.fixedness_cache = fixed.copy()
+
+    def _put_nonant_cache(self, cache):
+        """Flat scenario-major values into nonant_cache (spopt.py:530-543)."""
+        if getattr(self, "nonant_cache", None) is None:
+            raise RuntimeError("Rank {} Scenario {} nonant_cache is None (call _save_nonants first?)"
+                               .format(self.global_rank, self.local_scenario_names[0]))
+        S, N = self.nonant_cache.shape
+        assert len(cache) >= S * N
+        self.nonant_cache[:] = np.asarray(cache[:S * N], dtype=np.float64).reshape(S, N)
+
+    def _restore_nonants(self):
+        """Values and fixedness back from nonant_cache / fixedness_cache (spopt.py:638-662)."""
+        fixed, fv = self._fix_arrays()
+        fixed[:] = self.fixedness_cache
+        fv[:] = self.nonant_cache
+        self._fix_dirty = True
+        self._set_nonant_x(self.nonant_cache)
+
+    def _save_original_nonants(self):
+        """original_nonants / original_fixedness (spopt.py:690-710)."""
+        fixed, _ = self._fix_arrays()
+        self.original_nonants = np.ascontiguousarray(self._nonant_x())
+        self.original_fixedness = fixed.copy()
+
+    def _restore_original_nonants(self):
+        """spopt.py:713-741."""
+        fixed, fv = self._fix_arrays()
+        orig_fixed = getattr(self, "original_fixedness", None)
+        fixed[:] = False if orig_fixed is None else orig_fixed
+        fv[:] = self.original_nonants
+        self._fix_dirty = True
+        self._set_nonant_x(self.original_nonants)
+
+    def _restore_original_fixedness(self):
+        """Original fixedness, current values (spopt.py:546-554)."""
+        fixed, fv = self._fix_arrays()
+        orig = getattr(self, "original_fixedness", None)
+        new = np.zeros_like(fixed) if orig is None else orig
+        if not np.array_equal(new, fixed):
+            fv[:] = self._nonant_x()
+            fixed[:] = new
+            self._fix_dirty = True
+
+    def _unfix_nonants(self):
+        fixed, _ = self._fix_arrays()
+        if fixed.any():
+            fixed[:] = False
+            self._fix_dirty = True
+
+    def _apply_fixing(self):
+        """Upload per-scenario bounds with the fixed nonants (phx_set_bounds),
+        or restore the model's bounds when nothing is fixed."""
+        if not getattr(self, "_fix_dirty", False):
+            return
+        lib = self._native
+        fixed = self._fixed
+        if not fixed.any():
+            lib.check(self._ctx, lib.set_bounds(self._ctx, None, None, self._stream()), "set_bounds")
+            self._fix_lb = self._fix_ub = None
+        else:
+            b = self.batch
+            n, S = b.n, self._S
+            cols = torch.as_tensor(b.nonant.slot_col.astype(np.int64), device=self.device)
+            lb = self._dev["lb"].view(n, -1).expand(n, S).contiguous()
+            ub = self._dev["ub"].view(n, -1).expand(n, S).contiguous()
+            m = torch.as_tensor(np.ascontiguousarray(fixed.T), device=self.device)
+            v = torch.as_tensor(np.ascontiguousarray(self._fix_val.T), device=self.device)
+            lb[cols] = torch.where(m, v, lb[cols])
+            ub[cols] = torch.where(m, v, ub[cols])
+            lib.check(self._ctx, lib.set_bounds(self._ctx, lb.data_ptr(), ub.data_ptr(), self._stream()),
+                      "set_bounds")
+            self._fix_lb, self._fix_ub = lb, ub
+        self._fix_dirty = False

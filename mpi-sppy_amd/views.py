@@ -98,15 +98,56 @@ class _VarView:
         self._col = col
         self.name = name
 
+    def _slot(self):
+        return int(list(self._opt.batch.nonant.slot_col).index(self._col))
+
     @property
     def value(self):
         return float(self._opt._host("x")[self._col, self._s])
 
+    @value.setter
+    def value(self, v):
+        self._opt._host_write("x", self._col, self._s, v)
+
     _value = value
+
+    def set_value(self, v):
+        self.value = v
 
     @property
     def fixed(self):
-        return False
+        f = getattr(self._opt, "_fixed", None)
+        return bool(f is not None and f[self._s, self._slot()])
+
+    @fixed.setter
+    def fixed(self, flag):
+        if flag:
+            self.fix()
+        else:
+            self.unfix()
+
+    def is_fixed(self):
+        return self.fixed
+
+    def fix(self, value=None):
+        """Fix at ``value`` (or the current value), like Pyomo's VarData.fix."""
+        opt = self._opt
+        fixed, fv = opt._fix_arrays()
+        j = self._slot()
+        v = self.value if value is None else float(value)
+        if value is not None:
+            self.value = v
+        fixed[self._s, j] = True
+        fv[self._s, j] = v
+        opt._fix_dirty = True
+
+    def unfix(self):
+        opt = self._opt
+        fixed, _ = opt._fix_arrays()
+        j = self._slot()
+        if fixed[self._s, j]:
+            fixed[self._s, j] = False
+            opt._fix_dirty = True
 
     @property
     def stale(self):
@@ -174,6 +215,27 @@ class _DataNS:
     @property
     def has_variable_probability(self):
         return False
+
+    # per-scenario rows of the opt's [S_local][N] caches (writable numpy views)
+    def _cache_row(self, name):
+        a = getattr(self._view._opt, name, None)
+        return None if a is None else a[self._view._s]
+
+    @property
+    def nonant_cache(self):
+        return self._cache_row("nonant_cache")
+
+    @property
+    def fixedness_cache(self):
+        return self._cache_row("fixedness_cache")
+
+    @property
+    def original_nonants(self):
+        return self._cache_row("original_nonants")
+
+    @property
+    def original_fixedness(self):
+        return self._cache_row("original_fixedness")
 
 
 class ScenarioView:

@@ -210,3 +210,30 @@ def solve_ef(scens):
     x, status = qp.highs_solve(A, bl, bu, lb, ub, c)
     obj = float(np.dot(c, x)) + sum(s.prob * s.c0 for s in scens)
     return obj, x, status
+
+
+def evaluate_xhat(scens, cache, stage_max=None):
+    """``Xhat_Eval.evaluate`` (utils/xhat_eval.py:297-327) restated: fix each
+    scenario's nonants at ``cache[node][i]`` (lb = ub, spopt.py:557-591; only
+    stages <= stage_max when given, xhat_eval.py:331-366), solve the LP and
+    return (E[obj] = sum_s p_s obj_s, per-scenario objectives, feasible flags).
+    Probabilities are the scenarios' own (a ``num_scens`` smaller than the name
+    list makes them sum to more than 1, exactly as in the reference test)."""
+    S = len(scens)
+    objs = np.zeros(S)
+    feas = np.zeros(S, dtype=bool)
+    for k, s in enumerate(scens):
+        if s.prob is None:
+            s.prob = 1.0 / S
+        lb, ub = s.lb.copy(), s.ub.copy()
+        for (ndn, cp, st, vl) in s.nodes:
+            if stage_max is not None and st > stage_max:
+                continue
+            vals = cache[ndn]
+            for i, v in enumerate(vl):
+                lb[v] = ub[v] = float(vals[i])
+        x, ok = qp.solve(s.A, s.bl, s.bu, lb, ub, s.c, None)
+        feas[k] = ok
+        objs[k] = float(np.dot(s.c, x)) + s.c0 if ok else np.nan
+    E = math.fsum(s.prob * o for s, o in zip(scens, objs))
+    return E, objs, feas

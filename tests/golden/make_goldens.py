@@ -45,6 +45,16 @@ def main():
                              "objective": 970, "sig": 2}
     g["gradient_rho_iter0"] = {"source": "mpisppy/tests/test_gradient_rho.py (w_denom 25 = |x_scen0[CORN0]|)",
                                "scen0_x": {"CORN0": 25.0, "SUGAR_BEETS0": 375.0, "WHEAT0": 100.0}}
+    g["farmer_xhat_eval"] = {
+        "source": "mpisppy/tests/test_conf_int_farmer.py:63-76, 168-202 (Xhat_Eval over scen0..99 with "
+                  "num_scens=10, xhat ROOT=[74,245,181]; 2 sig)",
+        "names": 100, "num_scens": 10, "xhat_ROOT": [74.0, 245.0, 181.0],
+        "evaluate": -1300000.0, "evaluate_one_scen0": -48000.0, "sig": 2}
+    g["aircond_xhat_eval"] = {
+        "source": "mpisppy/tests/test_conf_int_aircond.py:38-93, 213-240 (BF [4,3,2], start_seed 0, "
+                  "xhat [200,0] at every non-leaf node; 2 sig, 'rebaselined feb 2022')",
+        "branching_factors": [4, 3, 2], "xhat_node": [200.0, 0.0],
+        "evaluate": 1000.0, "evaluate_one_scen0": 1100.0, "sig": 2}
     with open(os.path.join(HERE, "ref_goldens.json"), "w") as f:
         json.dump(g, f, indent=1)
 

@@ -115,3 +115,36 @@ def test_deferred_solve_with_stragglers_matches_sync(gpu_lib):
     assert any(s.get("stragglers", 0) > 0 for s in a.solve_stats)
     assert rel(a.W_array(), b.W_array()) < 1e-12
     assert rel(ca, cb) < 1e-12 and rel(Ea, Eb) < 1e-12 and rel(ta, tb_) < 1e-12
+
+
+def test_xhat_eval_farmer_gpu(gpu_lib):
+    """Xhat_Eval over farmer 100 names / num_scens 10 (test_conf_int_farmer.py:168-202)."""
+    from test_xhat_emu import check_farmer_xhat
+    check_farmer_xhat(gpu_lib, None)
+
+
+def test_xhat_eval_aircond_gpu(gpu_lib):
+    from test_xhat_emu import check_aircond_xhat
+    check_aircond_xhat(gpu_lib, None)
+
+
+def test_fixed_nonants_large_batch_gpu(gpu_lib):
+    """Fixing over 20k scenarios (generic path with per-scenario bounds), sampled
+    against the oracle; then unfixing returns to the lane path's solution."""
+    from mpisppy_amd.utils.xhat_eval import Xhat_Eval
+    from test_xhat_emu import xhat_options
+    S = 20000
+    ev = Xhat_Eval(xhat_options(), farmer.scenario_names_creator(S), farmer.scenario_creator,
+                   scenario_creator_kwargs={"num_scens": S}, _native_lib=gpu_lib)
+    ev.solve_loop()
+    base = ev.nonant_values().copy()
+    xhat = {"ROOT": [80.0, 250.0, 170.0]}
+    E = ev.evaluate(xhat)
+    assert ev.infeas_prob() == 0.0
+    idx = np.r_[0:5, S - 5:S, np.random.RandomState(0).choice(S, 20, replace=False)]
+    _, objs, _ = oph.evaluate_xhat([om.farmer("scen%d" % i, num_scens=S) for i in idx], xhat)
+    got = np.array([ev.objs_dict["scen%d" % i] for i in idx])
+    assert rel(got, objs) < 1e-9
+    ev._unfix_nonants()
+    ev.solve_loop()
+    assert rel(ev.nonant_values(), base) < 1e-9

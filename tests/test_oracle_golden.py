@@ -99,3 +99,26 @@ def test_conv_rank_emulation():
     sl = ph.rank_slices(S, 3)
     ref = sum(d[s].sum() / (len(s) * o.N) for s in sl) / 3
     assert o.convergence_diff() == pytest.approx(ref, rel=1e-15)
+
+
+def test_xhat_eval_farmer():
+    """Xhat_Eval.evaluate / evaluate_one (test_conf_int_farmer.py:168-202)."""
+    g = G["farmer_xhat_eval"]
+    scens = [models.farmer("scen%d" % i, num_scens=g["num_scens"]) for i in range(g["names"])]
+    E, objs, feas = ph.evaluate_xhat(scens, {"ROOT": g["xhat_ROOT"]})
+    assert feas.all()
+    assert round_pos_sig(E, g["sig"]) == g["evaluate"]
+    assert round_pos_sig(objs[0], g["sig"]) == g["evaluate_one_scen0"]
+
+
+def test_xhat_eval_aircond():
+    """Xhat_Eval.evaluate / evaluate_one, aircond (test_conf_int_aircond.py:213-240)."""
+    from mpisppy_amd.utils import sputils
+    g = G["aircond_xhat_eval"]
+    bf = g["branching_factors"]
+    scens = [models.aircond("scen%d" % i, bf, start_seed=0) for i in range(int(np.prod(bf)))]
+    cache = {nd: g["xhat_node"] for nd in sputils.create_nodenames_from_branching_factors(bf)}
+    E, objs, feas = ph.evaluate_xhat(scens, cache)
+    assert feas.all()
+    assert round_pos_sig(E, g["sig"]) == g["evaluate"]
+    assert round_pos_sig(objs[0], g["sig"]) == g["evaluate_one_scen0"]

@@ -1,0 +1,166 @@
+"""Nonant fixing (spopt.py:536-742) and Xhat_Eval (utils/xhat_eval.py) through the
+engine on CPU (test emulation of the C ABI), against the oracle's fixed-xhat
+evaluation and the reference's own Xhat_Eval asserts (ref_goldens.json).
+The GPU versions are in test_gpu_parity.py."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from helpers import ph_options, rel
+from mpisppy_amd.examples import aircond, farmer
+from mpisppy_amd.opt.ph import PH
+from mpisppy_amd.utils import sputils
+from mpisppy_amd.utils.xhat_eval import Xhat_Eval
+from oracle import models as om, ph as oph
+from test_oracle_golden import round_pos_sig
+
+G = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "ref_goldens.json")))
+
+
+def xhat_options(solver_options=None):
+    # test_conf_int_farmer.py:63-70
+    return {"iter0_solver_options": None, "iterk_solver_options": None, "display_timing": False,
+            "solver_name": "phx", "verbose": False, "solver_options": solver_options}
+
+
+def farmer_eval(lib, device, n_names=100, num_scens=10, solver_options=None):
+    return Xhat_Eval(xhat_options(solver_options), farmer.scenario_names_creator(n_names), farmer.scenario_creator,
+                     scenario_creator_kwargs={"num_scens": num_scens}, _native_lib=lib, _device=device)
+
+
+def check_farmer_xhat(lib, device):
+    g = G["farmer_xhat_eval"]
+    xhat = {"ROOT": np.array(g["xhat_ROOT"])}
+    ev = farmer_eval(lib, device, g["names"], g["num_scens"])
+    E = ev.evaluate(xhat)
+    Eo, objs, feas = oph.evaluate_xhat([om.farmer("scen%d" % i, num_scens=g["num_scens"])
+                                        for i in range(g["names"])], xhat)
+    assert rel(E, Eo) < 1e-9
+    assert round_pos_sig(E, g["sig"]) == g["evaluate"]
+    got = np.array([ev.objs_dict["scen%d" % i] for i in range(g["names"])])
+    assert rel(got, objs) < 1e-9
+    assert ev.infeas_prob() == 0.0
+    # the fixed nonants are the solution's nonants
+    assert np.array_equal(ev.nonant_values(), np.tile(xhat["ROOT"], (g["names"], 1)))
+    obj0 = ev.evaluate_one(xhat, "scen0", ev.local_scenarios["scen0"])
+    assert round_pos_sig(obj0, g["sig"]) == g["evaluate_one_scen0"]
+    assert rel(obj0, objs[0]) < 1e-9
+    # E[fct(obj)] (xhat_eval.py:218-263)
+    e2 = ev.Eobjective(fct=lambda v: np.array([v, v * v]))
+    p = 1.0 / g["num_scens"]
+    assert rel(e2, [p * objs.sum(), p * (objs ** 2).sum()]) < 1e-9
+
+
+def test_xhat_eval_farmer_emu(emu):
+    check_farmer_xhat(emu, "cpu")
+
+
+def check_aircond_xhat(lib, device):
+    g = G["aircond_xhat_eval"]
+    bf = g["branching_factors"]
+    S = int(np.prod(bf))
+    nodes = sputils.create_nodenames_from_branching_factors(bf)
+    ev = Xhat_Eval(xhat_options(), aircond.scenario_names_creator(S), aircond.scenario_creator,
+                   all_nodenames=nodes, scenario_creator_kwargs={"branching_factors": bf, "start_seed": 0},
+                   _native_lib=lib, _device=device)
+    cache = {nd: g["xhat_node"] for nd in nodes}
+    E = ev.evaluate(cache)
+    Eo, objs, feas = oph.evaluate_xhat([om.aircond("scen%d" % i, bf, start_seed=0) for i in range(S)], cache)
+    assert rel(E, Eo) < 1e-9
+    assert round_pos_sig(E, g["sig"]) == g["evaluate"]
+    obj0 = ev.evaluate_one(cache, "scen0", ev.local_scenarios["scen0"])
+    assert round_pos_sig(obj0, g["sig"]) == g["evaluate_one_scen0"]
+    # fix only stage 1 (fix_nonants_upto_stage), after unfixing everything
+    ev._unfix_nonants()
+    ev.fix_nonants_upto_stage(1, cache)
+    ev.solve_loop(compute_val_at_nonant=True)
+    E1 = ev.Eobjective()
+    Eo1, _, _ = oph.evaluate_xhat([om.aircond("scen%d" % i, bf, start_seed=0) for i in range(S)], cache,
+                                  stage_max=1)
+    assert rel(E1, Eo1) < 1e-9
+
+
+def test_xhat_eval_aircond_emu(emu):
+    check_aircond_xhat(emu, "cpu")
+
+
+def test_save_restore_fixedness_emu(emu):
+    """_save_nonants / _fix_nonants / _restore_nonants / _restore_original_fixedness
+    round trip: after restoring, the solve is the unfixed one again (lane path)."""
+    ev = farmer_eval(emu, "cpu", 12, 12)
+    ev.solve_loop()
+    base = ev.nonant_values().copy()
+    Ebase = ev.Eobjective()
+    ev._save_original_nonants()
+    ev._save_nonants()
+    assert np.array_equal(ev.local_scenarios["scen3"]._mpisppy_data.nonant_cache, base[3])
+    ev._fix_nonants({"ROOT": [100.0, 200.0, 200.0]})
+    view = ev.local_scenarios["scen0"]._mpisppy_data.nonant_indices
+    assert all(v.fixed for v in view.values())
+    ev.solve_loop()
+    assert np.array_equal(ev.nonant_values(), np.tile([100.0, 200.0, 200.0], (12, 1)))
+    ev._restore_nonants()
+    assert not any(v.fixed for v in view.values())
+    assert np.array_equal(ev.nonant_values(), base)
+    ev.solve_loop()
+    assert rel(ev.nonant_values(), base) < 1e-9
+    assert rel(ev.Eobjective(), Ebase) < 1e-12
+    # _put_nonant_cache + _restore_nonants (xhatshufflelooper_bounder.py:140-141)
+    ev._save_nonants()
+    flat = np.tile([120.0, 180.0, 200.0], 12)
+    ev._put_nonant_cache(flat)
+    ev._restore_nonants()
+    assert np.array_equal(ev.nonant_values(), flat.reshape(12, 3))
+    # per-variable fix through the views, then original fixedness
+    list(view.values())[0].fix(90.0)
+    ev.solve_loop()
+    assert ev.nonant_values()[0, 0] == 90.0
+    ev._restore_original_fixedness()
+    ev.solve_loop()
+    assert rel(ev.nonant_values(), base) < 1e-9
+
+
+def test_calculate_incumbent_and_infeasible_xhat_emu(emu):
+    ev = farmer_eval(emu, "cpu", 3, 3, solver_options={"pdhg_max_iters": 4096})
+    ev.solve_loop()
+    Elp = ev.Eobjective()
+    # each scenario fixed at its own LP optimum: same objective as the LP
+    inc = ev.calculate_incumbent()
+    assert inc is not None and rel(inc, Elp) < 1e-9
+    # an xhat over the 500-acre limit is infeasible in every scenario
+    ev.evaluate({"ROOT": [300.0, 300.0, 300.0]})
+    assert ev.infeas_prob() == pytest.approx(1.0)
+    ev._fix_nonants({"ROOT": [300.0, 300.0, 300.0]})
+    assert ev.calculate_incumbent(fix_nonants=False) is None
+
+
+def test_fix_errors_emu(emu):
+    ev = farmer_eval(emu, "cpu", 3, 3)
+    with pytest.raises(RuntimeError, match="Could not find"):
+        ev._fix_nonants({"ROOT_1": [1.0, 2.0, 3.0]})
+    with pytest.raises(RuntimeError, match="Needed 3 nonant Vars"):
+        ev._fix_nonants({"ROOT": [1.0, 2.0]})
+    with pytest.raises(RuntimeError, match="Empty cache"):
+        ev._fix_nonants({"ROOT": None})
+    with pytest.raises(RuntimeError, match="nonant_cache is None"):
+        ev._put_nonant_cache(np.zeros(9))
+
+
+def test_post_solve_bound_restores_original_fixedness_emu(emu):
+    """post_solve_bound unfixes (phbase.py:473-474): the Lagrangian bound with
+    W from PH equals the oracle's W-on/prox-off solve."""
+    names = farmer.scenario_names_creator(6)
+    ph = PH(ph_options(3), names, farmer.scenario_creator, scenario_creator_kwargs={"num_scens": 6},
+            _native_lib=emu, _device="cpu")
+    ph.ph_main()
+    W = ph.W_array()
+    ph._save_original_nonants()
+    ph._fix_nonants({"ROOT": [100.0, 200.0, 200.0]})
+    bound = ph.post_solve_bound()
+    o = oph.OraclePH([om.farmer(n, num_scens=6) for n in names], rho=1.0)
+    o.W = W.copy()
+    o.W_on, o.prox_on = 1, 0
+    o.solve_loop()
+    assert rel(bound, o.Ebound()) < 1e-9
