@@ -56,6 +56,10 @@ def parse():
     ap.add_argument("--cpu-scens", type=int, default=4000)
     ap.add_argument("--cpu-iters", type=int, default=3)
     ap.add_argument("--cpu-procs", type=int, default=16, help="worker processes (the GPU box's CPU share)")
+    ap.add_argument("--host-loop", action="store_true", help="drive each PH iteration from Python")
+    ap.add_argument("--depth", type=int, default=4, help="phx_iterk: iterations kept enqueued ahead")
+    ap.add_argument("--timing-every", type=int, default=5,
+                    help="phx_iterk: HIP events around the lane kernel of every T-th iteration")
     ap.add_argument("--conv", action="store_true", help="also measure time to conv < 1e-4")
     ap.add_argument("--conv-max-iters", type=int, default=5000)
     return ap.parse_args()
@@ -92,7 +96,7 @@ def pmc_traffic(kernel, args):
     import glob
     if args.scens != 100000 or args.cm != 1:
         return None, None
-    files = sorted(glob.glob(os.path.join(_ROOT, "profiles", "r*_pmc_%s.json" % kernel)))
+    files = sorted(glob.glob(os.path.join(_ROOT, "profiles", "r*_pmc_%s.json" % kernel.replace("phx_", ""))))
     if not files:
         return None, None
     d = json.load(open(files[-1]))
@@ -129,7 +133,8 @@ def main():
 
     S = args.scens
     names = farmer.scenario_names_creator(S)
-    solver_opts = {"pdhg_check_every": args.check_every, "lane_solver": args.lane_solver}
+    solver_opts = {"pdhg_check_every": args.check_every, "lane_solver": args.lane_solver,
+                   "iterk_depth": args.depth, "iterk_timing": args.timing_every}
     if args.ipm_after is not None:
         solver_opts["ipm_after"] = args.ipm_after
     if args.as_rounds is not None:
@@ -156,30 +161,58 @@ def main():
     ph.Iter0()
     torch.cuda.synchronize()
     t_iter0 = time.perf_counter() - t_iter0
-    for _ in range(args.warmup):
-        step()
-    ph._settle()
-    n0 = len(ph.solve_stats)
-    ph.mpicomm.Barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    ph._settle()                 # the last solve may be deferred: finish it inside the timed region
-    torch.cuda.synchronize()
-    ph.mpicomm.Barrier()
-    dt = time.perf_counter() - t0
+    K = args.steps
+    b = ph.batch
+    if args.host_loop:
+        # one PHBase method call after the other from Python (the reference's loop body)
+        for _ in range(args.warmup):
+            step()
+        ph._settle()
+        n0 = len(ph.solve_stats)
+        ph.mpicomm.Barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(K):
+            step()
+        ph._settle()             # the last solve may be deferred: finish it inside the timed region
+        torch.cuda.synchronize()
+        ph.mpicomm.Barrier()
+        dt = time.perf_counter() - t0
+        stats = ph.solve_stats[n0:]
+        lane_warm_ms = sum(s.get("lane_warm_ms", 0.0) for s in stats)
+        warm_launches = sum(1 for s in stats if s.get("lane_warm_ms", 0.0) > 0.0)
+        loop_info = {"loop": "host (PHBase methods per iteration, deferred solves)"}
+    else:
+        # PHBase.iterk_loop itself: with no per-iteration hooks it runs on the
+        # device (phx_iterk: pipelined iterations, device-side stop test)
+        ph.options["PHIterLimit"] = args.warmup
+        ph.iterk_loop()
+        torch.cuda.synchronize()
+        ph.options["PHIterLimit"] = K
+        ph.mpicomm.Barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ph.iterk_loop()
+        torch.cuda.synchronize()
+        ph.mpicomm.Barrier()
+        dt = time.perf_counter() - t0
+        st = getattr(ph, "iterk_stats", None)
+        if st is None or st["iters"] != K or st["solves"] != K:
+            raise RuntimeError("timed iterk_loop did not run %d full iterations: %s" % (K, st))
+        stats = []
+        lane_warm_ms = st["lane_warm_ms"]
+        warm_launches = st["warm_launches"]
+        loop_info = {"loop": "PHBase.iterk_loop -> phx_iterk (device-driven, depth %d)" % args.depth,
+                     "straggler_stops": st["straggler_stops"], "stragglers": st["stragglers"],
+                     "not_optimal": st["not_optimal"]}
     dt_t = torch.tensor([dt], dtype=torch.float64, device="cuda")
     ph.mpicomm.allreduce_max_(dt_t)
     dt = float(dt_t.item())
-    stats = ph.solve_stats[n0:]
-    b = ph.batch
-    K = args.steps
-    lane_on = any(s.get("lane_ms", 0.0) > 0.0 for s in stats)
+    lane_on = lane_warm_ms > 0.0
     if lane_on:
         # dominant kernel: the warm active-set lane kernel, one launch per step over all local scenarios
-        k_ms = sum(s.get("lane_warm_ms", 0.0) for s in stats)
-        launches = sum(1 for s in stats if s.get("lane_warm_ms", 0.0) > 0.0)
+        k_ms = lane_warm_ms
+        launches = warm_launches
         bpu = lane_bytes(b)
         units_per_launch = b.S
         kernel = "phx_lane_warm"
@@ -218,7 +251,8 @@ def main():
                      "unit_def": "scenario solve" if lane_on else "scenario PDHG iteration",
                      "units_per_launch": units_per_launch,
                      "avg_launch_us": avg_launch_s * 1e6, "launches": launches},
-        "kernel_ms_per_step": {"lane_warm": sum(s.get("lane_warm_ms", 0.0) for s in stats) / K,
+        "loop": loop_info,
+        "kernel_ms_per_step": {"lane_warm": lane_warm_ms / K,
                                "lane_warm_list": sum(s.get("lane_warm_list_ms", 0.0) for s in stats) / K,
                                "lane_cold": sum(s.get("lane_ms", 0.0) for s in stats) / K,
                                "pdhg": sum(s["pdhg_ms"] for s in stats) / K,
@@ -226,9 +260,10 @@ def main():
                                "ipm": sum(s["ipm_ms"] for s in stats) / K},
         "lane_certified_per_step": [s.get("lane_certified") for s in stats],
         "lane_warm_certified_per_step": [s.get("lane_warm_certified") for s in stats],
+        "lane_first_certified_per_step": [s.get("lane_first_certified") for s in stats],
         "pdhg_iters_per_step": [s["pdhg_iters"] for s in stats],
         "solver_options": solver_opts,
-        "not_optimal": sum(s["not_optimal"] for s in stats),
+        "not_optimal": sum(s["not_optimal"] for s in stats) if stats else loop_info.get("not_optimal"),
         "setup_s": t_setup, "iter0_s": t_iter0,
     }
     if args.conv:

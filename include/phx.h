@@ -114,6 +114,8 @@ typedef struct phx_solve_stats {
     int32_t stragglers;       /* lanes the lane solver handed to the generic
                                  path (their x was final only after it)       */
     int32_t jit;              /* 1 if this context has a specialised kernel   */
+    int32_t lane_first_certified; /* certified by the first lane pass (the
+                                 affine-map pass when maps are on)            */
 } phx_solve_stats;
 
 /* Scenario-tree reduction layout for Compute_Xbar (phbase.py:27-107): for each
@@ -233,6 +235,63 @@ int phx_expect(phx_ctx* ctx, const double* prob, const double* obj,
 int phx_export_slots(phx_ctx* ctx, const double* src, double* out, void* stream);
 
 int phx_last_solve_stats(const phx_ctx* ctx, phx_solve_stats* out_host);
+
+/* In-place SUM all-reduce of `count` doubles at device `buf` over the ranks,
+ * ordered on `stream` (the caller's collective: RCCL through torch.distributed
+ * on the GPU).  Returns 0 on success.                                        */
+typedef int (*phx_allreduce_fn)(void* user, double* buf, int64_t count, void* stream);
+
+/* The PH main loop after Iter0 (PHBase.iterk_loop, phbase.py:875-979) for
+ * runs without per-iteration host hooks (no extensions, converger or hub):
+ * per iteration k = 1..max_iters
+ *     Compute_Xbar -> [allreduce] -> Update_W -> convergence_diff -> stop if
+ *     conv < convthresh (before the solve, phbase.py:914-926) -> solve
+ * with the stop test evaluated ON THE DEVICE: the host keeps `depth`
+ * iterations enqueued ahead, a device flag turns the kernels of iterations
+ * past the stop into no-ops, and the host only polls a mapped progress word
+ * (no per-iteration host round trip).  A solve that leaves lanes to the
+ * generic path stops the pipeline at the next Update_W (all ranks alike: the
+ * count travels in the all-reduced node sums); the host finishes those lanes
+ * and resumes, so every iteration sees final x exactly as the Python loop.
+ * Requires the lane solver (phx_jit_info "on"), no phx_set_bounds override,
+ * a finished previous solve, and segments that partition the local
+ * scenarios.  W is updated in place.  The PH terms are those of the last
+ * phx_set_ph_terms (W, rho, xbar_node must be the arrays given here).       */
+typedef struct phx_iterk_args {
+    double* x; double* y; double* obj; int32_t* status; int32_t* iters;   /* solve outputs */
+    const phx_tree_desc* tree; const double* prob_coeff; double* partial;
+    double* node_sums;               /* [2*NNS] xbar | xsqbar, published once an iteration proceeds */
+    double* node_stage;              /* [2*NNS+1] this iteration's sums (+ straggler count); the
+                                        buffer the all-reduce callback receives              */
+    const int32_t* xbar_idx; const double* rho; double* W;
+    int32_t nseg; const int32_t* seg_s0_host; const int32_t* seg_s1_host; double* seg_sums;
+    const double* conv_counts_host;  /* [nseg] element count of each emulated rank (all ranks) */
+    int32_t conv_R;                  /* emulated rank count (phbase.py:330-343) */
+    double convthresh;
+    int32_t max_iters;               /* iterations to run at most                */
+    int32_t depth;                   /* iterations kept enqueued ahead (>= 1)    */
+    int32_t timing;                  /* T > 0: HIP events around the phx_lane_warm launch of
+                                        every T-th iteration (each record costs ~6 us of GPU
+                                        time, so the sample is sparse); 0: none            */
+    phx_allreduce_fn allreduce;      /* NULL on one rank                         */
+    void* allreduce_user;
+} phx_iterk_args;
+
+typedef struct phx_iterk_result {
+    int32_t iters;         /* the reference's _PHIter at loop exit              */
+    int32_t converged;     /* 1: conv < convthresh at iteration `iters` (no solve then) */
+    double conv;           /* convergence_diff of iteration `iters`             */
+    int32_t solves;        /* solves completed                                  */
+    int32_t straggler_stops; /* pipeline stops to finish generic-path lanes      */
+    int32_t stragglers;    /* lanes finished on the generic path, total         */
+    int32_t not_optimal;   /* lanes left uncertified by the last solve          */
+    double warm_ms;        /* sum of phx_lane_warm durations (timing = 1)       */
+    int32_t warm_launches;
+    double wall_ms;
+} phx_iterk_result;
+
+int phx_iterk(phx_ctx* ctx, const phx_solve_opts* opts, const phx_iterk_args* args,
+              phx_iterk_result* result_host, void* stream);
 
 /* Human-readable state of the structure-specialised lane solver for this
  * context ("on: ..." or "off: <reason>").                                   */

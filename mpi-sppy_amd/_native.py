@@ -50,6 +50,7 @@ class SolveStats(ctypes.Structure):
         ("lane_warm_ms", c_double), ("lane_warm_list_ms", c_double),
         ("lane_iters", c_double), ("pdhg_launches", c_int32), ("total_iters", c_int32),
         ("lane_certified", c_int32), ("lane_warm_certified", c_int32), ("not_optimal", c_int32), ("stragglers", c_int32), ("jit", c_int32),
+        ("lane_first_certified", c_int32),
     ]
 
 
@@ -64,10 +65,35 @@ class TreeDesc(ctypes.Structure):
     ]
 
 
+ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, c_void_p, c_void_p, ctypes.c_int64, c_void_p)
+
+
+class IterkArgs(ctypes.Structure):
+    _fields_ = [
+        ("x", c_void_p), ("y", c_void_p), ("obj", c_void_p), ("status", c_void_p), ("iters", c_void_p),
+        ("tree", ctypes.POINTER(TreeDesc)), ("prob_coeff", c_void_p), ("partial", c_void_p),
+        ("node_sums", c_void_p), ("node_stage", c_void_p),
+        ("xbar_idx", c_void_p), ("rho", c_void_p), ("W", c_void_p),
+        ("nseg", c_int32), ("seg_s0_host", c_void_p), ("seg_s1_host", c_void_p), ("seg_sums", c_void_p),
+        ("conv_counts_host", c_void_p), ("conv_R", c_int32), ("convthresh", c_double),
+        ("max_iters", c_int32), ("depth", c_int32), ("timing", c_int32),
+        ("allreduce", ALLREDUCE_FN), ("allreduce_user", c_void_p),
+    ]
+
+
+class IterkResult(ctypes.Structure):
+    _fields_ = [
+        ("iters", c_int32), ("converged", c_int32), ("conv", c_double), ("solves", c_int32),
+        ("straggler_stops", c_int32), ("stragglers", c_int32), ("not_optimal", c_int32),
+        ("warm_ms", c_double), ("warm_launches", c_int32), ("wall_ms", c_double),
+    ]
+
+
 # every symbol of include/phx.h (tests check the library exports all of them)
 SYMBOLS = [
     "create", "destroy", "last_error", "build_info", "set_problem", "set_bounds", "set_ph_terms",
     "solve", "solve_finish", "objective", "xbar", "update_w", "expect", "export_slots", "last_solve_stats", "jit_info",
+    "iterk",
 ]
 
 
@@ -116,6 +142,8 @@ class Lib:
         self.export_slots = fn("export_slots", ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p])
         self.last_solve_stats = fn("last_solve_stats", ctypes.c_int, [c_void_p, ctypes.POINTER(SolveStats)])
         self.jit_info = fn("jit_info", ctypes.c_char_p, [c_void_p])
+        self.iterk = fn("iterk", ctypes.c_int, [c_void_p, ctypes.POINTER(SolveOpts), ctypes.POINTER(IterkArgs),
+                                                ctypes.POINTER(IterkResult), c_void_p])
 
     def check(self, ctx, rc, what):
         if rc != 0:

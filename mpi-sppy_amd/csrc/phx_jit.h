@@ -196,14 +196,24 @@ inline std::string lane_kernel_source(const LaneStructure& L, int warm_waves = 1
     // one of its lanes needs a second round.
     o << "extern \"C\" __global__ void __launch_bounds__(64, " << warm_waves
       << ") phx_lane_warm(phx_lane::LaneIO io) {\n"
+         "  if (phx_lane::gated(io.gate)) return;\n"
          "  phx_lane::zero_next_counts(io.counts_next);\n"
          "  const int t = blockIdx.x * 64 + threadIdx.x;\n"
          "  bool still = false;\n"
          "  if (t < io.S) still = phx_lane::warm_lane<PT>(io, t);\n"
          "  phx_lane::compact_lane(still, t, io.lanes_out, io.count_out);\n"
          "}\n";
+    o << "extern \"C\" __global__ void __launch_bounds__(64, 4) phx_lane_map(phx_lane::LaneIO io) {\n"
+         "  if (phx_lane::gated(io.gate)) return;\n"
+         "  phx_lane::zero_next_counts(io.counts_next);\n"
+         "  const int t = blockIdx.x * 64 + threadIdx.x;\n"
+         "  bool still = false;\n"
+         "  if (t < io.S) still = phx_lane::map_lane<PT>(io, t);\n"
+         "  phx_lane::compact_lane(still, t, io.lanes_out, io.count_out);\n"
+         "}\n";
     o << "extern \"C\" __global__ void __launch_bounds__(64, " << warm_waves
       << ") phx_lane_warm_list(phx_lane::LaneIO io, const int* lanes, const int* count) {\n"
+         "  if (phx_lane::gated(io.gate)) return;\n"
          "  const int nl = *count;\n"
          "  for (int base = blockIdx.x * 64; base < nl; base += gridDim.x * 64) {\n"
          "    const int t = base + threadIdx.x;\n"
@@ -215,6 +225,7 @@ inline std::string lane_kernel_source(const LaneStructure& L, int warm_waves = 1
          "}\n";
     o << "extern \"C\" __global__ void __launch_bounds__(64) phx_lane_cold(phx_lane::LaneIO io, "
          "const int* lanes, const int* count) {\n"
+         "  if (phx_lane::gated(io.gate)) return;\n"
          "  phx_lane::zero_next_counts(io.counts_next);\n"
          "  const int nl = count ? *count : io.S;\n"
          "  for (int base = blockIdx.x * 64; base < nl; base += gridDim.x * 64) {\n"

@@ -89,6 +89,7 @@ constexpr int KKT_REFINE = 6;
 // flags bits shared with the host / generic path
 constexpr int32_t FLAG_IPM_TRIED = 1;   // interior point already attempted
 constexpr int32_t FLAG_WRITTEN = 2;     // outputs written by a lane kernel
+constexpr int32_t FLAG_MAP = 4;         // the lane's affine map (LaneIO::map) matches its stored active set
 
 // Runtime inputs/outputs (device pointers; per-scenario arrays [i*S + s]).
 // A, c, bounds below are scaled iff PT::scaled() (phx_jit.h LaneStructure).
@@ -134,7 +135,13 @@ struct LaneIO {
     int32_t refine;
     int32_t as_rounds;     // active-set rounds after the interior point (phx_lane_cold)
     int32_t warm_rounds;   // active-set rounds per warm pass
+    const int32_t* gate;   // *gate != 0: the launch does nothing (phx_iterk past its stop), or null
+    double* map;           // [map_words<PT>()][S] affine solution maps (see map_apply), or null
 };
+
+// phx_iterk gate: every kernel of an iteration past the device-side stop exits
+// at once (one scalar load; the counters stay as the last real solve left them)
+PHX_LD bool gated(const int32_t* gate) { return gate && *(const volatile int32_t*)gate; }
 
 // Data access for one lane: scenario-varying numbers in registers; the
 // invariant ones are literals of the specialised kernel (PT tables), which the
@@ -673,51 +680,70 @@ PHX_LD void classify(const Data<PT>& D, const double* xv, const double* yv, doub
 // from the given (xp, z) (a proximal-point iteration that converges to the
 // KKT solution nearest the start on degenerate faces).  Non-free columns are
 // set to their bound.  false if the Schur complement is not positive definite.
+// Factor of one active set: Schur complement A_RF (P_FF + reg)^-1 A_RF' + reg I
+// (inactive rows: identity), packed Cholesky, and 1/(p + reg) of the nonant
+// columns.
 template <class PT>
-PHX_LD bool kkt_solve(const Data<PT>& D, const ASet<PT>& a, double* xp, double* z) {
-    constexpr int NN = PT::NMAX_N, MM = PT::NMAX_M, TT = PT::NMAX_M * (PT::NMAX_M + 1) / 2;
+struct KFactor {
+    double M[PT::NMAX_M * (PT::NMAX_M + 1) / 2], idg[PT::NMAX_M];
+    double ipn[PT::NMAX_S];
+    PHX_LD double Hinv(int j) const { return PT::col_slot(j) >= 0 ? ipn[PT::col_slot(j)] : 1.0 / KKT_REG; }
+};
+
+template <class PT>
+PHX_LD bool kkt_factor(const Data<PT>& D, const ASet<PT>& a, KFactor<PT>& K) {
+    constexpr int TT = PT::NMAX_M * (PT::NMAX_M + 1) / 2;
     constexpr double reg = KKT_REG;
     // 1/(p_j + reg): a literal for columns without a PH slot (p = 0), three
     // or so reciprocals for the nonant columns; masked by F(j) where needed
-    double ipn[PT::NMAX_S];
     PHX_UNROLL for (int j = 0; j < PT::n(); ++j)
-        if (PT::col_slot(j) >= 0) ipn[PT::col_slot(j)] = 1.0 / (D.p(j) + reg);
-    auto Hinv = [&](int j) { return PT::col_slot(j) >= 0 ? ipn[PT::col_slot(j)] : 1.0 / reg; };
-    double M[TT], idg[MM];
-    PHX_UNROLL for (int j = 0; j < PT::n(); ++j)
-        if (!a.F(j)) xp[j] = a.up(j) ? D.u(j) : D.l(j);
-    PHX_UNROLL for (int i = 0; i < PT::m(); ++i) if (!a.R(i)) z[i] = 0.0;
-    PHX_UNROLL for (int t = 0; t < TT; ++t) M[t] = 0.0;
-    PHX_UNROLL for (int i = 0; i < PT::m(); ++i) M[tri(i, i)] = a.R(i) ? reg : 1.0;
+        if (PT::col_slot(j) >= 0) K.ipn[PT::col_slot(j)] = 1.0 / (D.p(j) + reg);
+    PHX_UNROLL for (int t = 0; t < TT; ++t) K.M[t] = 0.0;
+    PHX_UNROLL for (int i = 0; i < PT::m(); ++i) K.M[tri(i, i)] = a.R(i) ? reg : 1.0;
     PHX_UNROLL for (int t = 0; t < PT::npairs(); ++t) {
         const int ka = PT::pair_a(t), kb = PT::pair_b(t);
         if (a.R(PT::row(ka)) && a.R(PT::row(kb)) && a.F(PT::col(ka)))
-            M[PT::pair_pos(t)] += D.A(ka) * Hinv(PT::col(ka)) * D.A(kb);
+            K.M[PT::pair_pos(t)] += D.A(ka) * K.Hinv(PT::col(ka)) * D.A(kb);
     }
-    if (!cholesky<PT>(M, idg)) { PHX_LANE_FAIL(10, -1); return false; }
+    if (!cholesky<PT>(K.M, K.idg)) { PHX_LANE_FAIL(10, -1); return false; }
+    return true;
+}
+
+// Iterative refinement on the regularised system from (xp, z) towards the KKT
+// solution for the right-hand side given by R: R.q(j) linear term, R.xb(j)
+// value of a non-free column, R.b(i) the active side of row i (a
+// proximal-point iteration: it converges to the solution nearest the start on
+// degenerate faces).
+template <class PT, class RHS>
+PHX_LD void kkt_refine(const Data<PT>& D, const ASet<PT>& a, const KFactor<PT>& K, const RHS& R, double* xp,
+                       double* z) {
+    constexpr int NN = PT::NMAX_N, MM = PT::NMAX_M;
+    PHX_UNROLL for (int j = 0; j < PT::n(); ++j)
+        if (!a.F(j)) xp[j] = R.xb(j);
+    PHX_UNROLL for (int i = 0; i < PT::m(); ++i) if (!a.R(i)) z[i] = 0.0;
     PHX_REFINE_LOOP for (int it = 0; it < KKT_REFINE; ++it) {
         double r1[NN], t[MM];
         {
             double atz[NN];
             D.matvec_t(z, atz);
             PHX_UNROLL for (int j = 0; j < PT::n(); ++j)
-                r1[j] = a.F(j) ? -D.q(j) - D.p(j) * xp[j] - atz[j] : 0.0;
+                r1[j] = a.F(j) ? -R.q(j) - D.p(j) * xp[j] - atz[j] : 0.0;
         }
         {
             double axp[MM], hr[NN], ahr[MM];
             D.matvec(xp, axp);
-            PHX_UNROLL for (int j = 0; j < PT::n(); ++j) hr[j] = r1[j] * Hinv(j);   // r1 = 0 off F
+            PHX_UNROLL for (int j = 0; j < PT::n(); ++j) hr[j] = r1[j] * K.Hinv(j);   // r1 = 0 off F
             D.matvec(hr, ahr);
             PHX_UNROLL for (int i = 0; i < PT::m(); ++i)
-                t[i] = a.R(i) ? ahr[i] - ((a.lo(i) ? D.bl(i) : D.bu(i)) - axp[i]) : 0.0;
+                t[i] = a.R(i) ? ahr[i] - (R.b(i) - axp[i]) : 0.0;
         }
-        chol_solve_inv<PT>(M, idg, t);
+        chol_solve_inv<PT>(K.M, K.idg, t);
         double atdz[NN];
         D.matvec_t(t, atdz);
         double dmax = 0.0, xmax = 0.0;
         PHX_UNROLL for (int j = 0; j < PT::n(); ++j)
             if (a.F(j)) {
-                const double d = (r1[j] - atdz[j]) * Hinv(j);
+                const double d = (r1[j] - atdz[j]) * K.Hinv(j);
                 xp[j] += d;
                 dmax = fmax(dmax, fabs(d));
                 xmax = fmax(xmax, fabs(xp[j]));
@@ -730,6 +756,101 @@ PHX_LD bool kkt_solve(const Data<PT>& D, const ASet<PT>& a, double* xp, double* 
             }
         PHX_LANE_STAT(1);
         if (dmax <= 1e-10 * (1.0 + xmax)) break;
+    }
+}
+
+// right-hand sides: the lane's own problem; the affine parts of the map
+template <class PT>
+struct RhsFull {
+    const Data<PT>& D;
+    const ASet<PT>& a;
+    PHX_LD double q(int j) const { return D.q(j); }
+    PHX_LD double xb(int j) const { return a.up(j) ? D.u(j) : D.l(j); }
+    PHX_LD double b(int i) const { return a.lo(i) ? D.bl(i) : D.bu(i); }
+};
+template <class PT>
+struct RhsBase {      // the PH terms off: q = c
+    const Data<PT>& D;
+    const ASet<PT>& a;
+    PHX_LD double q(int j) const { return D.c(j); }
+    PHX_LD double xb(int j) const { return a.up(j) ? D.u(j) : D.l(j); }
+    PHX_LD double b(int i) const { return a.lo(i) ? D.bl(i) : D.bu(i); }
+};
+template <class PT>
+struct RhsSlot {      // d/dqn[t]: unit linear term on slot t's column, homogeneous otherwise
+    const Data<PT>& D;
+    int t;
+    PHX_LD double q(int j) const { return PT::col_slot(j) == t ? D.dc(j) : 0.0; }
+    PHX_LD double xb(int) const { return 0.0; }
+    PHX_LD double b(int) const { return 0.0; }
+};
+
+// Equality-constrained KKT solve for the active set a:
+//      [ P_FF   A_RF' ] [x_F]   [ -q_F        ]
+//      [ A_RF   0     ] [ z ] = [ b_R - A_RB x_B ]     (z = -y_R)
+// by its quasi-definite regularisation (P+reg, -reg) and iterative refinement
+// from the given (xp, z).  Non-free columns are set to their bound.  false if
+// the Schur complement is not positive definite.
+template <class PT>
+PHX_LD bool kkt_solve(const Data<PT>& D, const ASet<PT>& a, double* xp, double* z) {
+    KFactor<PT> K;
+    if (!kkt_factor<PT>(D, a, K)) return false;
+    kkt_refine<PT>(D, a, K, RhsFull<PT>{D, a}, xp, z);
+    return true;
+}
+
+// ---------------------------------------------------------------------------
+// Affine solution map of one active set.  With the active set and the prox
+// weights p fixed, the KKT solution is affine in the nonant linear terms qn:
+//      (x, z) = (x0, z0) + sum_t qn[t] (gx_t, gz_t)
+// PH changes only qn (W and x-bar) from one iteration to the next, and after
+// the first few iterations the active set stays put, so a warm solve becomes
+// this evaluation plus the KKT certificate — no factorisation, no refinement.
+// Stored per lane (scenario-minor words): [x0 (n) | z0 (m) | gx,gz per slot |
+// p per slot]; trusted when FLAG_MAP is set and p is bitwise the same.
+// ---------------------------------------------------------------------------
+template <class PT>
+PHX_LD constexpr int map_words() { return (PT::n() + PT::m()) * (PT::nslot() + 1) + PT::nslot(); }
+
+template <class PT>
+PHX_LD bool map_compute(const Data<PT>& D, const ASet<PT>& a, const LaneIO& io, int sc) {
+    constexpr int NN = PT::NMAX_N, MM = PT::NMAX_M;
+    const int64_t S = io.S;
+    const int W = PT::n() + PT::m();
+    KFactor<PT> K;
+    if (!kkt_factor<PT>(D, a, K)) return false;
+    PHX_NOUNROLL for (int t = -1; t < PT::nslot(); ++t) {
+        double xp[NN], z[MM];
+        PHX_UNROLL for (int j = 0; j < PT::n(); ++j) xp[j] = 0.0;
+        PHX_UNROLL for (int i = 0; i < PT::m(); ++i) z[i] = 0.0;
+        if (t < 0) kkt_refine<PT>(D, a, K, RhsBase<PT>{D, a}, xp, z);
+        else kkt_refine<PT>(D, a, K, RhsSlot<PT>{D, t}, xp, z);
+        double* m = io.map + (int64_t)(t + 1) * W * S + sc;
+        PHX_UNROLL for (int j = 0; j < PT::n(); ++j) m[(int64_t)j * S] = xp[j];
+        PHX_UNROLL for (int i = 0; i < PT::m(); ++i) m[(int64_t)(PT::n() + i) * S] = z[i];
+    }
+    double* mp = io.map + (int64_t)(PT::nslot() + 1) * W * S + sc;
+    PHX_UNROLL for (int t = 0; t < PT::nslot(); ++t) mp[(int64_t)t * S] = D.pn[t];
+    return true;
+}
+
+// (x, z) from the map; false if the map does not apply (different p)
+template <class PT>
+PHX_LD bool map_apply(const Data<PT>& D, const LaneIO& io, int sc, double* xp, double* z) {
+    const int64_t S = io.S;
+    const int W = PT::n() + PT::m();
+    const double* mp = io.map + (int64_t)(PT::nslot() + 1) * W * S + sc;
+    bool same = true;
+    PHX_UNROLL for (int t = 0; t < PT::nslot(); ++t) same = same && mp[(int64_t)t * S] == D.pn[t];
+    if (!same) return false;
+    const double* m0 = io.map + sc;
+    PHX_UNROLL for (int j = 0; j < PT::n(); ++j) xp[j] = m0[(int64_t)j * S];
+    PHX_UNROLL for (int i = 0; i < PT::m(); ++i) z[i] = m0[(int64_t)(PT::n() + i) * S];
+    PHX_UNROLL for (int t = 0; t < PT::nslot(); ++t) {
+        const double q = D.qn[t];
+        const double* mt = io.map + (int64_t)(t + 1) * W * S + sc;
+        PHX_UNROLL for (int j = 0; j < PT::n(); ++j) xp[j] += q * mt[(int64_t)j * S];
+        PHX_UNROLL for (int i = 0; i < PT::m(); ++i) z[i] += q * mt[(int64_t)(PT::n() + i) * S];
     }
     return true;
 }
@@ -817,7 +938,7 @@ PHX_LD bool as_rounds(const Data<PT>& D, ASet<PT>& a, const LaneIO& io, int roun
 // Certified lane: unscaled outputs, objective (incl. PH terms), active set.
 template <class PT>
 PHX_LD void write_certified(const LaneIO& io, const Data<PT>& D, int sc, const ASet<PT>& a, const double* xp,
-                            const double* z, int its) {
+                            const double* z, int its, bool map_ok = false) {
     const int S = io.S;
     double f = D.kn;
     PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
@@ -833,7 +954,7 @@ PHX_LD void write_certified(const LaneIO& io, const Data<PT>& D, int sc, const A
     io.iters[sc] = its;
     if (io.status_out) io.status_out[sc] = 1;
     if (io.iters_out) io.iters_out[sc] = its;
-    io.flags[sc] = its > 0 ? (FLAG_WRITTEN | FLAG_IPM_TRIED) : FLAG_WRITTEN;
+    io.flags[sc] = (its > 0 ? (FLAG_WRITTEN | FLAG_IPM_TRIED) : FLAG_WRITTEN) | (map_ok ? FLAG_MAP : 0);
     aset_store<PT>(io, sc, a);
 }
 
@@ -849,11 +970,48 @@ PHX_LD bool warm_lane(const LaneIO& io, int sc) {
     double xp[NN], z[MM];
     PHX_UNROLL for (int j = 0; j < PT::n(); ++j) xp[j] = 0.0;
     PHX_UNROLL for (int i = 0; i < PT::m(); ++i) z[i] = 0.0;
+    if (io.map && (io.flags[sc] & FLAG_MAP) && map_apply<PT>(D, io, sc, xp, z)) {
+        PHX_LANE_STAT(2);
+        // the same active set, so the same certificate as a KKT solve's
+        const int c = certify_update<PT>(D, a, xp, z, io.kkt_tol);
+        if (c == 0) {
+            write_certified<PT>(io, D, sc, a, xp, z, 0, true);
+            return false;
+        }
+        // the active set moved: rounds from the updated set, warm from (xp, z)
+    }
     if (as_rounds<PT>(D, a, io, io.warm_rounds, xp, z)) {
-        write_certified<PT>(io, D, sc, a, xp, z, 0);
+        const bool mok = io.map && map_compute<PT>(D, a, io, sc);
+        write_certified<PT>(io, D, sc, a, xp, z, 0, mok);
         return false;
     }
     aset_store<PT>(io, sc, a);   // the updated active set seeds the next pass
+    io.status[sc] = 0;
+    io.flags[sc] = 0;
+    return true;
+}
+
+// Affine-map pass (phx_lane_map): the lane's stored map evaluated and
+// certified; nothing else, so the kernel stays small (registers, occupancy)
+// and streams the maps.  true: the lane goes on to the rounds pass.
+template <class PT>
+PHX_LD bool map_lane(const LaneIO& io, int sc) {
+    constexpr int NN = PT::NMAX_N, MM = PT::NMAX_M;
+    if (io.flags[sc] & FLAG_MAP) {
+        const Data<PT> D(io, sc);
+        double xp[NN], z[MM];
+        if (map_apply<PT>(D, io, sc, xp, z)) {
+            PHX_LANE_STAT(2);
+            ASet<PT> a;
+            aset_load<PT>(io, sc, a);
+            const int c = certify_update<PT>(D, a, xp, z, io.kkt_tol);
+            if (c == 0) {
+                write_certified<PT>(io, D, sc, a, xp, z, 0, true);
+                return false;
+            }
+            aset_store<PT>(io, sc, a);   // the rounds pass starts from the updated set
+        }
+    }
     io.status[sc] = 0;
     io.flags[sc] = 0;
     return true;
@@ -875,7 +1033,8 @@ PHX_LD bool cold_lane(const LaneIO& io, int sc) {
         PHX_UNROLL for (int j = 0; j < PT::n(); ++j) xp[j] = x[j];
         PHX_UNROLL for (int i = 0; i < PT::m(); ++i) z[i] = a.R(i) ? -y[i] : 0.0;
         if (as_rounds<PT>(D, a, io, io.as_rounds, xp, z)) {
-            write_certified<PT>(io, D, sc, a, xp, z, its > 0 ? its : 1);
+            const bool mok = io.map && map_compute<PT>(D, a, io, sc);
+            write_certified<PT>(io, D, sc, a, xp, z, its > 0 ? its : 1, mok);
             return false;
         }
     }

@@ -17,6 +17,7 @@ Device mapping:
                     (phbase.py:330-343)
   solve_loop        phx_set_ph_terms + phx_solve (batched PDHG + KKT polish)
 """
+import ctypes
 import math
 import time
 
@@ -351,6 +352,96 @@ class PHBase(SPOpt):
         self.current_solver_options = self.options["iterk_solver_options"]
         return self.trivial_bound
 
+    def _native_loop_ok(self):
+        """The device-driven loop (phx_iterk) runs the same iterations when no
+        per-iteration host hook or printout needs the host between steps."""
+        o = self.options
+        if self.extensions is not None or self.ph_converger is not None or self.spcomm is not None:
+            return False
+        if o["display_progress"] or o["verbose"] or o["display_convergence_detail"]:
+            return False
+        so = self.current_solver_options or {}
+        if not int(so.get("native_loop", 1)) or not int(self._solve_opts(so).lane_solver):
+            return False
+        if getattr(self, "_fixed", None) is not None and self._fixed.any():
+            return False
+        if self.NNS == 0 or self.batch.nonant.N == 0:
+            return False
+        return not self._native.jit_info(self._ctx).decode().startswith("off")
+
+    def _allreduce_cb(self):
+        if getattr(self, "_ar_cb", None) is None:
+            bufs = {self._node_stage.data_ptr(): self._node_stage, self._seg_sums.data_ptr(): self._seg_sums}
+            comm = self.mpicomm
+
+            def cb(user, ptr, count, stream):
+                try:
+                    comm.allreduce_(bufs[ptr][:count])
+                    return 0
+                except Exception as e:   # reported by phx_iterk as a failed all-reduce
+                    print("phx_iterk all-reduce callback failed:", repr(e))
+                    return 1
+            self._ar_cb = _native.ALLREDUCE_FN(cb)
+        return self._ar_cb
+
+    def _iterk_native(self, max_iterations):
+        """iterk_loop body on the device (phx_iterk): Compute_Xbar -> Update_W ->
+        convergence_diff -> stop test -> solve_loop, pipelined with a device-side
+        stop flag (phbase.py:875-979 semantics, same kernels as the host loop)."""
+        self._settle()
+        self._apply_fixing()
+        self._set_ph_terms()
+        lib = self._native
+        so_dict = self.current_solver_options or {}
+        so = self._solve_opts(so_dict)
+        so.defer = 0
+        a = getattr(self, "_iterk_args", None)
+        if a is None:
+            a = _native.IterkArgs()
+            a.x, a.y, a.obj = self._x.data_ptr(), self._y.data_ptr(), self._obj.data_ptr()
+            a.status, a.iters = self._status.data_ptr(), self._iters.data_ptr()
+            a.tree = ctypes.pointer(self._tree)
+            a.prob_coeff, a.partial = self._pc.data_ptr(), self._partial.data_ptr()
+            a.node_sums, a.node_stage = self._node_buf.data_ptr(), self._node_stage.data_ptr()
+            a.xbar_idx = self._xbar_idx_t.data_ptr()
+            a.nseg = len(self._conv_seg)
+            a.seg_s0_host = ctypes.cast(self._seg_s0, ctypes.c_void_p)
+            a.seg_s1_host = ctypes.cast(self._seg_s1, ctypes.c_void_p)
+            a.seg_sums = self._seg_sums.data_ptr()
+            self._conv_counts_c = (ctypes.c_double * len(self._conv_counts))(*self._conv_counts)
+            a.conv_counts_host = ctypes.cast(self._conv_counts_c, ctypes.c_void_p)
+            a.conv_R = self._conv_R
+            if self.n_proc > 1:
+                a.allreduce = self._allreduce_cb()
+            self._iterk_args = a
+        a.rho, a.W = self._rho.data_ptr(), self._W.data_ptr()
+        a.convthresh = float(self.options["convthresh"])
+        a.max_iters = int(max_iterations)
+        a.depth = int(so_dict.get("iterk_depth", 4))
+        a.timing = int(so_dict.get("iterk_timing", 0))
+        res = _native.IterkResult()
+        t0 = time.perf_counter()
+        lib.check(self._ctx, lib.iterk(self._ctx, ctypes.byref(so), ctypes.byref(a), ctypes.byref(res),
+                                       self._stream()), "iterk")
+        wall = time.perf_counter() - t0
+        self._bump()
+        self._PHIter = int(res.iters)
+        self.conv = float(res.conv) if res.iters > 0 else None
+        self._conv_cache = self._seg_sums
+        self._conv_value = self.conv
+        self._conv_updated_w = True
+        self.iter_times = [wall / max(res.iters, 1)] * int(res.iters)
+        self.iterk_stats = {"iters": int(res.iters), "converged": bool(res.converged), "solves": int(res.solves),
+                            "straggler_stops": int(res.straggler_stops), "stragglers": int(res.stragglers),
+                            "not_optimal": int(res.not_optimal), "lane_warm_ms": float(res.warm_ms),
+                            "warm_launches": int(res.warm_launches), "wall_s": wall}
+        if res.not_optimal:
+            stc = self._status.cpu().numpy()
+            name = self.__class__.__name__
+            for k in np.nonzero(stc != 1)[0][:10]:
+                print("[%s] Solve failed for scenario %s" % (name, self.local_scenario_names[k]))
+        return res
+
     def iterk_loop(self):
         """phbase.py:875-979."""
         verbose = self.options["verbose"]
@@ -361,6 +452,13 @@ class PHBase(SPOpt):
         self.conv = None
         max_iterations = int(self.options["PHIterLimit"])
         self.iter_times = []
+        if self._native_loop_ok():
+            res = self._iterk_native(max_iterations)
+            if not res.converged:
+                self.mpicomm.Barrier()
+                if self.cylinder_rank == 0 and (dprogress or verbose):
+                    _global_toc("Reached user-specified limit=%d on number of PH iterations" % max_iterations)
+            return
         for self._PHIter in range(1, max_iterations + 1):
             iteration_start_time = time.time()
             if dprogress and self.cylinder_rank == 0:

@@ -179,7 +179,8 @@ class SPOpt(SPBase):
                     "lane_iters": stt.lane_iters, "polish_ms": stt.polish_ms, "ipm_ms": stt.ipm_ms,
                     "lane_ms": stt.lane_ms, "lane_warm_ms": stt.lane_warm_ms,
                     "lane_warm_list_ms": stt.lane_warm_list_ms, "lane_certified": stt.lane_certified,
-                    "lane_warm_certified": stt.lane_warm_certified, "stragglers": stragglers,
+                    "lane_warm_certified": stt.lane_warm_certified,
+                    "lane_first_certified": stt.lane_first_certified, "stragglers": stragglers,
                     "wall_s": time.perf_counter() - t0, "not_optimal": n_bad})
         if n_bad and gripe:
             stc = self._status.cpu().numpy()

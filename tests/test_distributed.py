@@ -32,21 +32,26 @@ def _worker(rank, world, port, out, case):
     from mpisppy_amd.examples import aircond, farmer
     from mpisppy_amd.utils import sputils
     emu = _native.Lib(os.path.join(ROOT, "tests", "emu", "libphx_emu.so"), prefix="emu_phx_")
+    case, loop = case.split("-")
+    # native: the device-driven loop (phx_iterk, all-reduce through the
+    # callback); host: the Python loop (PHBase methods one by one)
+    opts = {"iterk_solver_options": {"native_loop": 1 if loop == "native" else 0}}
     if case == "farmer":
         ph, conv, Eobj, tb = run_engine(farmer.scenario_creator, farmer.scenario_names_creator(9),
-                                        {"num_scens": 9}, 4, lib=emu, device="cpu", mpicomm=Comm())
+                                        {"num_scens": 9}, 4, lib=emu, device="cpu", mpicomm=Comm(), options=opts)
     else:
         bfs = [3, 2, 2]
         ph, conv, Eobj, tb = run_engine(aircond.scenario_creator, ["scen%d" % i for i in range(12)],
                                         {"branching_factors": bfs, "start_seed": 0}, 3, lib=emu, device="cpu",
-                                        mpicomm=Comm(),
+                                        mpicomm=Comm(), options=opts,
                                         all_nodenames=sputils.create_nodenames_from_branching_factors(bfs))
+    assert ph._iterk_args is not None if loop == "native" else not hasattr(ph, "_iterk_args")
     out[rank] = (conv, Eobj, tb, ph.W_array(), {k: v[0] for k, v in ph.xbar_by_node().items()})
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("case", ["farmer", "aircond"])
+@pytest.mark.parametrize("case", ["farmer-native", "farmer-host", "aircond-native", "aircond-host"])
 def test_two_ranks_match_one(emu, case):
     from helpers import run_engine
     from mpisppy_amd.examples import aircond, farmer
@@ -54,7 +59,7 @@ def test_two_ranks_match_one(emu, case):
     mgr = mp.Manager()
     out = mgr.dict()
     mp.spawn(_worker, args=(2, _free_port(), out, case), nprocs=2, join=True)
-    if case == "farmer":
+    if case.startswith("farmer"):
         ph, conv, Eobj, tb = run_engine(farmer.scenario_creator, farmer.scenario_names_creator(9), {"num_scens": 9},
                                         4, lib=emu, device="cpu", options={"conv_ranks": 2})
     else:

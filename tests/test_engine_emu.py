@@ -147,7 +147,7 @@ def test_deferred_solve_with_stragglers_matches_sync(emu, so):
     S = 24
     runs = []
     for defer in (1, 0):
-        o = dict(so, defer=defer)
+        o = dict(so, defer=defer, native_loop=0)
         ph, conv, Eobj, tb = run_engine(farmer.scenario_creator, farmer.scenario_names_creator(S),
                                         {"num_scens": S}, 4, lib=emu, device="cpu",
                                         options={"iter0_solver_options": o, "iterk_solver_options": o})
@@ -157,3 +157,44 @@ def test_deferred_solve_with_stragglers_matches_sync(emu, so):
     assert np.array_equal(a.W_array(), b.W_array())
     assert np.array_equal(a.xbar_by_node()["ROOT"][0], b.xbar_by_node()["ROOT"][0])
     assert ca == cb and Ea == Eb and ta == tb_
+
+
+@pytest.mark.parametrize("case", ["farmer", "aircond", "conv_ranks", "converge"])
+def test_native_loop_matches_host_loop_emu(emu, case):
+    """phx_iterk (device-driven iterk_loop) against the Python loop of PHBase
+    methods: the same iterations, bit for bit."""
+    check_native_vs_host(emu, "cpu", case)
+
+
+def check_native_vs_host(lib, device, case, S=30, solver=None):
+    runs = []
+    for nl in (1, 0):
+        so = dict(solver or {}, native_loop=nl)
+        opts = {"iter0_solver_options": dict(solver or {}), "iterk_solver_options": so}
+        kw = dict(lib=lib, device=device, options=opts)
+        if case == "aircond":
+            bfs = [3, 3, 2]
+            r = run_engine(aircond.scenario_creator, ["scen%d" % i for i in range(18)],
+                           {"branching_factors": bfs, "start_seed": 0}, 5,
+                           all_nodenames=sputils.create_nodenames_from_branching_factors(bfs), **kw)
+        else:
+            iters = 400 if case == "converge" else 5
+            if case == "conv_ranks":
+                opts["conv_ranks"] = 4
+            if case == "converge":
+                opts["convthresh"] = 1e-3
+                S = 30                   # converges within the 400 iterations
+            r = run_engine(farmer.scenario_creator, farmer.scenario_names_creator(S), {"num_scens": S}, iters,
+                           **kw)
+        runs.append(r)
+    (a, ca, Ea, ta), (b, cb, Eb, tb_) = runs
+    assert hasattr(a, "iterk_stats") and not hasattr(b, "iterk_stats")
+    assert a._PHIter == b._PHIter
+    if case == "converge":
+        assert a.iterk_stats["converged"] and a._PHIter < 400
+    assert np.array_equal(a.W_array(), b.W_array())
+    assert np.array_equal(a.nonant_values(), b.nonant_values())
+    for k, v in b.xbar_by_node().items():
+        assert np.array_equal(a.xbar_by_node()[k][0], v[0])
+    assert ca == cb and Ea == Eb and ta == tb_
+    return a, b

@@ -105,7 +105,7 @@ def test_deferred_solve_with_stragglers_matches_sync(gpu_lib):
     so = {"as_rounds": 0, "ipm_max_it": 2}
     runs = []
     for defer in (1, 0):
-        o = dict(so, defer=defer)
+        o = dict(so, defer=defer, native_loop=0)
         ph, conv, Eobj, tb = run_engine(farmer.scenario_creator, farmer.scenario_names_creator(S),
                                         {"num_scens": S}, 4, lib=gpu_lib,
                                         options={"iter0_solver_options": o, "iterk_solver_options": o})
@@ -148,3 +148,32 @@ def test_fixed_nonants_large_batch_gpu(gpu_lib):
     ev._unfix_nonants()
     ev.solve_loop()
     assert rel(ev.nonant_values(), base) < 1e-9
+
+
+@pytest.mark.parametrize("case", ["farmer", "aircond", "conv_ranks", "converge"])
+def test_native_loop_matches_host_loop_gpu(gpu_lib, case):
+    """phx_iterk (device-side stop flag, pipelined) == the Python loop, bit for bit."""
+    from test_engine_emu import check_native_vs_host
+    check_native_vs_host(gpu_lib, None, case, S=1000)
+
+
+@pytest.mark.parametrize("so", [{"as_rounds": 0, "ipm_max_it": 2}, {"as_rounds": 1, "ipm_max_it": 3}])
+def test_native_loop_straggler_stops_gpu(gpu_lib, so):
+    """Starved lane solves leave lanes to the generic path: phx_iterk stops the
+    pipeline, finishes them and resumes; the trajectory equals the host loop's."""
+    from test_engine_emu import check_native_vs_host
+    a, b = check_native_vs_host(gpu_lib, None, "farmer", S=2000, solver=so)
+    assert a.iterk_stats["straggler_stops"] > 0
+
+
+def test_affine_map_path_matches_oracle_gpu(gpu_lib, monkeypatch):
+    """Opt-in affine solution maps (PHX_LANE_MAP=1, phx_lane.h map_apply): the
+    map pass + rounds pass give the oracle's PH trajectory."""
+    monkeypatch.setenv("PHX_LANE_MAP", "1")
+    S = 300
+    ph, conv, Eobj, tb = run_engine(farmer.scenario_creator, farmer.scenario_names_creator(S), {"num_scens": S},
+                                    6, lib=gpu_lib)
+    o = oph.OraclePH([om.farmer("scen%d" % i, num_scens=S) for i in range(S)], rho=1.0)
+    oc, oE, otb = o.ph_main(6)
+    assert rel(ph.W_array(), o.W) < 1e-7
+    assert rel(conv, oc) < 1e-7 and rel(Eobj, oE) < 1e-9 and rel(tb, otb) < 1e-9
