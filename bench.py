@@ -2,7 +2,8 @@
 
 A "step" is one PH iteration over every scenario (Compute_Xbar -> Update_W ->
 convergence_diff -> batched subproblem solve), i.e. the body of
-``PHBase.iterk_loop`` (mpisppy/phbase.py:901-970).  Workload: farmer,
+``PHBase.iterk_loop`` (mpisppy/phbase.py:901-970); the timed region is
+``iterk_loop`` itself running K iterations (on the device: phx_iterk).  Workload: farmer,
 crops_multiplier 1, 100,000 synthetic scenarios (configs[2] of BASELINE.json;
 the metric is quoted on it and it fits one MI355X), rho = 1, scenarios sharded
 contiguously over the ranks (strong scaling: the 100k total is fixed).
@@ -10,14 +11,15 @@ contiguously over the ranks (strong scaling: the 100k total is fixed).
     python bench.py [--gpus N] [--steps K] [--warmup W] [--scens S] [--cm C]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
 
-Timed region: K steps bracketed by barrier + device synchronize; the MAX over
-ranks is reported.  Iter0 and the W warmup steps are untimed.  Inputs are
+Timed region: iterk_loop with PHIterLimit = K bracketed by barrier + device
+synchronize; the MAX over ranks is reported.  Iter0 and W warmup iterations are
+untimed.  --host-loop drives the iterations from Python instead.  Inputs are
 resident in HBM before timing.  Extra keys:
   roofline      the dominant kernel of the timed region (the structure-
                 specialised lane solver ``phx_lane_warm`` with the lane solver
                 on, the PDHG chunk ``k_chunk`` otherwise): algorithmic bytes
                  / its average duration from HIP events recorded
-                on the solve stream inside phx_solve.
+                around it on the solve stream (every --timing-every-th iteration).
   cpu_baseline  the CPU restatement of the reference PH (oracle/cpu_bench.py:
                 numpy + scipy-HiGHS + polish, one worker process per core) on a
                 bounded sample, run as a child process on rank 0 at N = 1.
@@ -53,8 +55,8 @@ def parse():
     ap.add_argument("--lane-solver", type=int, default=1, help="1: structure-specialised lane solver first")
     ap.add_argument("--as-rounds", type=int, default=None, help="active-set rounds (0: no warm active set)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-scens", type=int, default=4000)
-    ap.add_argument("--cpu-iters", type=int, default=3)
+    ap.add_argument("--cpu-scens", type=int, default=40000)
+    ap.add_argument("--cpu-iters", type=int, default=6)
     ap.add_argument("--cpu-procs", type=int, default=16, help="worker processes (the GPU box's CPU share)")
     ap.add_argument("--host-loop", action="store_true", help="drive each PH iteration from Python")
     ap.add_argument("--depth", type=int, default=4, help="phx_iterk: iterations kept enqueued ahead")
@@ -163,7 +165,7 @@ def main():
     t_iter0 = time.perf_counter() - t_iter0
     K = args.steps
     b = ph.batch
-    if args.host_loop:
+    if args.host_loop or not ph._native_loop_ok():
         # one PHBase method call after the other from Python (the reference's loop body)
         for _ in range(args.warmup):
             step()
@@ -252,7 +254,8 @@ def main():
                      "units_per_launch": units_per_launch,
                      "avg_launch_us": avg_launch_s * 1e6, "launches": launches},
         "loop": loop_info,
-        "kernel_ms_per_step": {"lane_warm": lane_warm_ms / K,
+        # lane_warm: average sampled launch (one launch per step)
+        "kernel_ms_per_step": {"lane_warm": lane_warm_ms / max(warm_launches, 1) if not stats else lane_warm_ms / K,
                                "lane_warm_list": sum(s.get("lane_warm_list_ms", 0.0) for s in stats) / K,
                                "lane_cold": sum(s.get("lane_ms", 0.0) for s in stats) / K,
                                "pdhg": sum(s["pdhg_ms"] for s in stats) / K,

@@ -121,7 +121,10 @@ typedef struct phx_solve_stats {
 /* Scenario-tree reduction layout for Compute_Xbar (phbase.py:27-107): for each
  * tile, the nonant slots [slot_lo, slot_lo+nlen) of one tree node summed over
  * the contiguous local scenarios [s_begin, s_end).  Tiles of one node are
- * consecutive; node_tile_ptr[v]..node_tile_ptr[v+1] lists them.             */
+ * consecutive; node_tile_ptr[v]..node_tile_ptr[v+1] lists them, and their
+ * partial offsets are consecutive too: tile_out[t] = tile_out[t0] +
+ * (t - t0) * 2 * nlen for the tiles t0.. of one node.  Tiles of at most 256
+ * scenarios (one per thread of a 256-thread block).                         */
 typedef struct phx_tree_desc {
     int32_t ntiles;
     const int32_t* tile_s0;    /* [ntiles] */

@@ -85,6 +85,10 @@ PHX_LD constexpr int aset_words(int n, int m) { return (2 * (n + m) + 31) / 32; 
 // 1/(p+reg) of the LP columns folds to a constant).
 constexpr double KKT_REG = 1e-6;
 constexpr int KKT_REFINE = 6;
+#ifndef PHX_KKT_STOP
+#define PHX_KKT_STOP 1e-10
+#endif
+constexpr double KKT_STOP = PHX_KKT_STOP;
 
 // flags bits shared with the host / generic path
 constexpr int32_t FLAG_IPM_TRIED = 1;   // interior point already attempted
@@ -755,7 +759,10 @@ PHX_LD void kkt_refine(const Data<PT>& D, const ASet<PT>& a, const KFactor<PT>& 
                 xmax = fmax(xmax, fabs(z[i]));
             }
         PHX_LANE_STAT(1);
-        if (dmax <= 1e-10 * (1.0 + xmax)) break;
+        // stop once the correction vanishes (1e-10 relative): the certificate's
+        // tolerance is relative to the problem's scale, so it cannot stand in
+        // for this (a looser stop, 1e-5, passed certificates at 1e-7 accuracy)
+        if (dmax <= KKT_STOP * (1.0 + xmax)) break;
     }
 }
 

@@ -226,7 +226,7 @@ class SPBase:
             xbar_idx[j] = node_off[node_id[t]] + nn.slot_local[j]
         self._xbar_idx = xbar_idx
         # tiles for the segmented xbar reduction
-        CH = int(self.options.get("xbar_tile", 1024))
+        CH = int(self.options.get("xbar_tile", 256))
         slot_lo = [int(np.argmax(nn.slot_stage == t + 1)) for t in range(T)]
         tiles = []   # (node v, s0, s1, slot0, nlen)
         for t in range(T):

@@ -19,6 +19,42 @@ __global__ __launch_bounds__(RED_NT) void v_loads(int S, const int32_t* slot_col
     for (int j = 0; j < 3; ++j) a += pc[ix(j, s, S)] * x[ix(slot_col[j], s, S)];
     out[s] = a;
 }
+// variant: 1 scenario per thread, 391 blocks, block_sum_multi of 6 values, partial per block
+__global__ __launch_bounds__(256) void v_tiles256(int S, const int32_t* slot_col, const double* x, const double* pc,
+                                                  double* partial) {
+    __shared__ double sh[4 * 8];
+    const int s = blockIdx.x * 256 + threadIdx.x;
+    double acc[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] = 0.0;
+    if (s < S) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const double xv = x[ix(slot_col[j], s, S)];
+            const double v = pc[ix(j, s, S)] * xv;
+            acc[j] = v; acc[4 + j] = v * xv;
+        }
+    }
+    block_sum_multi<256, 8>(acc, sh);
+    if (threadIdx.x == 0) for (int k = 0; k < 8; ++k) partial[blockIdx.x * 8 + k] = acc[k];
+}
+// variant: 4 scen/thread, no block reduction (thread partials written)
+__global__ __launch_bounds__(256) void v_noreduce(int S, const int32_t* slot_col, const double* x, const double* pc,
+                                                  double* out) {
+    double acc[6] = {0, 0, 0, 0, 0, 0};
+    for (int u = 0; u < 4; ++u) {
+        const int s = blockIdx.x * 1024 + threadIdx.x + u * 256;
+        if (s < S)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                const double xv = x[ix(slot_col[j], s, S)];
+                const double v = pc[ix(j, s, S)] * xv;
+                acc[j] += v; acc[3 + j] += v * xv;
+            }
+    }
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    if (acc[0] + acc[1] + acc[2] + acc[3] + acc[4] + acc[5] == 12345.0) out[t] = 0.0;
+}
 __global__ void v_empty(int S, double* out) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s < 0) out[s] = 0;
@@ -27,7 +63,7 @@ __global__ void v_empty(int S, double* out) {
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("err %s line %d\n", hipGetErrorString(e), __LINE__); return 1; } } while (0)
 
 int main() {
-    const int S = 100000, n = 12, N = 3, CH = 1024;
+    const int S = 100000, n = 12, N = 3, CH = 256;
     std::vector<int32_t> slot_col = {0, 1, 2};
     double *x, *pc, *partial, *node, *W, *rho, *seg, *out;
     int32_t *sc, *xi;
@@ -60,7 +96,7 @@ int main() {
     int32_t *d0 = up(t0), *d1 = up(t1), *dsl = up(tsl), *dnl = up(tnl), *dout = up(tout), *dptr = up(nptr), *doff = up(noff), *dnnl = up(nnl);
     std::vector<int32_t> sp = {0, nt};
     int32_t* dsp = up(sp);
-    unsigned int* tick; CK(hipMalloc(&tick, 16)); CK(hipMemset(tick, 0, 16));
+    unsigned int* tick; CK(hipMalloc(&tick, 8 * TICKET_SET)); CK(hipMemset(tick, 0, 8 * TICKET_SET));
     hipStream_t st; CK(hipStreamCreate(&st));
     hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     auto timeit = [&](const char* name, auto launch) {
@@ -76,9 +112,11 @@ int main() {
     };
     timeit("empty (391 blocks x 256)", [&] { hipLaunchKernelGGL(v_empty, dim3(391), dim3(256), 0, st, S, out); });
     timeit("loads only (391 x 256, 1 scen/thread)", [&] { hipLaunchKernelGGL(v_loads, dim3(391), dim3(256), 0, st, S, sc, x, pc, out); });
+    timeit("xbar 1 scen/thread + block_sum_multi (391 x 256)", [&] { hipLaunchKernelGGL(v_tiles256, dim3(391), dim3(256), 0, st, S, sc, x, pc, partial); });
+    timeit("xbar 4 scen/thread, no block reduce (98 x 256)", [&] { hipLaunchKernelGGL(v_noreduce, dim3(98), dim3(256), 0, st, S, sc, x, pc, out); });
     timeit("xbar tiles only (98 x 256)", [&] { hipLaunchKernelGGL(v_tiles, dim3(nt), dim3(RED_NT), 0, st, S, d0, d1, dsl, dnl, dout, sc, x, pc, partial); });
-    timeit("k_xbar full", [&] { hipLaunchKernelGGL(k_xbar, dim3(nt), dim3(RED_NT), 0, st, S, nt, d0, d1, dsl, dnl, dout, sc, x, pc, partial, 1, dptr, doff, dnnl, 3, node, tick, (const int32_t*)nullptr, (const int32_t*)nullptr); });
-    timeit("k_update_w_seg full", [&] { hipLaunchKernelGGL(k_update_w_seg, dim3(nt), dim3(RED_NT), 0, st, N, S, sc, x, (const double*)node, xi, rho, (const double*)W, W, 1, (double*)nullptr, d0, d1, partial, 1, dsp, seg, tick + 1, IterkCtl{}); });
-    timeit("k_update_w_seg no W update", [&] { hipLaunchKernelGGL(k_update_w_seg, dim3(nt), dim3(RED_NT), 0, st, N, S, sc, x, (const double*)node, xi, rho, (const double*)W, W, 0, (double*)nullptr, d0, d1, partial, 1, dsp, seg, tick + 1, IterkCtl{}); });
+    timeit("k_xbar full", [&] { hipLaunchKernelGGL(k_xbar, dim3(nt), dim3(RED_NT), 0, st, S, nt, d0, d1, dsl, dnl, dout, sc, x, pc, partial, 1, dptr, doff, dnnl, 3, node, tick, (const int32_t*)nullptr, (const int32_t*)nullptr, 1); });
+    timeit("k_update_w_seg full", [&] { hipLaunchKernelGGL(k_update_w_seg, dim3(nt), dim3(RED_NT), 0, st, N, S, sc, x, (const double*)node, xi, rho, (const double*)W, W, 1, (double*)nullptr, d0, d1, partial, 1, dsp, seg, tick + TICKET_SET, IterkCtl{}); });
+    timeit("k_update_w_seg no W update", [&] { hipLaunchKernelGGL(k_update_w_seg, dim3(nt), dim3(RED_NT), 0, st, N, S, sc, x, (const double*)node, xi, rho, (const double*)W, W, 0, (double*)nullptr, d0, d1, partial, 1, dsp, seg, tick + TICKET_SET, IterkCtl{}); });
     return 0;
 }
