@@ -177,3 +177,13 @@ def test_affine_map_path_matches_oracle_gpu(gpu_lib, monkeypatch):
     oc, oE, otb = o.ph_main(6)
     assert rel(ph.W_array(), o.W) < 1e-7
     assert rel(conv, oc) < 1e-7 and rel(Eobj, oE) < 1e-9 and rel(tb, otb) < 1e-9
+
+
+def test_hub_contract_gpu(gpu_lib):
+    from test_hub_spoke_emu import check_hub
+    check_hub(gpu_lib, None, S=300)
+
+
+def test_lagrangian_spoke_gpu(gpu_lib):
+    from test_hub_spoke_emu import check_lagrangian_spoke
+    check_lagrangian_spoke(gpu_lib, None, S=300)
