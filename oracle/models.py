@@ -14,6 +14,7 @@ Nonant order follows ``scenario_tree.build_vardatalist`` (``scenario_tree.py:11-
 indexed Vars are expanded in ``sorted(keys)`` (string sort for farmer),
 scalar Vars keep the given order.
 """
+import os
 import re
 import numpy as np
 
@@ -242,3 +243,51 @@ def aircond_nodenames(branching_factors):
         names += nxt
         frontier = nxt
     return names
+
+
+# ---------------------------------------------------------------- sslp
+_SSLP_JSON = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "mpi-sppy_amd", "examples",
+                          "data", "sslp_15_45.json")
+
+
+def sslp(sname, instance=None, num_scens=None):
+    """sslp LP relaxation (``examples/sslp/model/ReferenceModel.py``): FacilityOpen,
+    Allocation in [0,1], Dummy >= 0; demand rows sum_i D_ij A_ij - Dummy_j - Cap Open_j <= 0,
+    client rows sum_j A_ij == ClientPresent_i.  Data from the reference's .dat files
+    (extracted to sslp_15_45.json); unshipped scenarios draw ClientPresent ~
+    Bernoulli(0.5) from RandomState(K)."""
+    import json
+    d = json.load(open(_SSLP_JSON))
+    ns, nc = d["NumServers"], d["NumClients"]
+    K = extract_num(sname)
+    shipped = d["ClientPresent"].get(str(instance)) if instance is not None else None
+    if shipped is not None and 1 <= K <= len(shipped):
+        present = np.array(shipped[K - 1], dtype=np.float64)
+    else:
+        present = (np.random.RandomState(K).rand(nc) < 0.5).astype(np.float64)
+    n = ns + nc * ns + ns
+    names = ["FacilityOpen[%d]" % (j + 1) for j in range(ns)]
+    names += ["Allocation[(%d, %d)]" % (i + 1, j + 1) for i in range(nc) for j in range(ns)]
+    names += ["Dummy[%d]" % (j + 1) for j in range(ns)]
+    c = np.zeros(n)
+    lb = np.zeros(n)
+    ub = np.ones(n)
+    ub[ns + nc * ns:] = INF
+    A = np.zeros((ns + nc, n))
+    bl = np.zeros(ns + nc)
+    bu = np.zeros(ns + nc)
+    for j in range(ns):
+        c[j] = d["FixedCost"][j]
+        c[ns + nc * ns + j] = d["Penalty"]
+        A[j, j] = -d["Capacity"]
+        A[j, ns + nc * ns + j] = -1.0
+        for i in range(nc):
+            A[j, ns + i * ns + j] = d["Demand"][i][j]
+        bl[j], bu[j] = -INF, 0.0
+    for i in range(nc):
+        for j in range(ns):
+            c[ns + i * ns + j] = -d["Revenue"][i][j]
+            A[ns + i, ns + i * ns + j] = 1.0
+        bl[ns + i] = bu[ns + i] = present[i]
+    prob = 1.0 / num_scens if num_scens is not None else None
+    return Scen(sname, names, c, 0.0, A, bl, bu, lb, ub, [("ROOT", 1.0, 1, list(range(ns)))], prob)

@@ -187,3 +187,20 @@ def test_hub_contract_gpu(gpu_lib):
 def test_lagrangian_spoke_gpu(gpu_lib):
     from test_hub_spoke_emu import check_lagrangian_spoke
     check_lagrangian_spoke(gpu_lib, None, S=300)
+
+
+def test_sslp_ph_gpu(gpu_lib):
+    """sslp_15_45_5 LP relaxation (n = 705, m = 60: generic PDHG + polish path) vs the oracle."""
+    from test_sslp import check_sslp_ph
+    check_sslp_ph(gpu_lib, None, iters=3)
+
+
+def test_sslp_synthetic_batch_gpu(gpu_lib):
+    """400 synthetic sslp scenarios (batch creator): every subproblem certified, the
+    trivial bound equal to the oracle's."""
+    from mpisppy_amd.examples import sslp
+    names = sslp.scenario_names_creator(400)
+    ph, conv, Eobj, tb = run_engine(sslp.scenario_creator, names, {}, 1, lib=gpu_lib)
+    assert all(s["not_optimal"] == 0 for s in ph.solve_stats)
+    o = oph.OraclePH([om.sslp(nm) for nm in names], rho=1.0)
+    assert rel(tb, o.iter0()) < 1e-8

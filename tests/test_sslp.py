@@ -1,0 +1,60 @@
+"""sslp LP relaxation (workload C5a): the restated scenario creator
+(batch == per-scenario models, bit-exact), and PH through the engine (generic
+PDHG + polish path: n = 705 is above the lane-solver limits) against the oracle on
+the shipped sslp_15_45_5 instance.  The reference ships no sslp golden values
+(no sslp test in mpisppy/tests): parity here is engine vs the oracle restatement,
+whose PH loop is pinned by the farmer/aircond goldens (test_oracle_golden.py)."""
+import numpy as np
+import pytest
+
+from helpers import rel, run_engine
+from mpisppy_amd.batch import from_models
+from mpisppy_amd.examples import sslp
+from oracle import models as om, ph as oph
+
+
+def test_sslp_batch_equals_models():
+    names = sslp.scenario_names_creator(8)          # Scenario1..5 shipped, 6..8 synthetic
+    a = from_models(names, [sslp.scenario_creator(nm, instance=5) for nm in names]).compress()
+    b = sslp.batch_creator(names, instance=5).compress()
+    for k in ["rowptr", "colidx", "kvar", "Aconst", "Avar", "c", "lb", "ub", "bl", "bu"]:
+        assert np.array_equal(getattr(a, k), getattr(b, k)), k
+    assert (a.n, a.m, a.nnz) == (705, 60, b.nnz)
+    assert list(a.nonant.slot_col) == list(range(15)) and a.rhs_vary and not a.c_vary
+    # the shipped instance data, and the synthetic Bernoulli(0.5) rate
+    d = sslp.data()
+    assert np.array_equal(a.bl[:, 15:][0], d["ClientPresent"]["5"][0])
+    P = np.stack([sslp.client_present(k) for k in range(100, 400)])
+    assert 0.45 < P.mean() < 0.55
+
+
+def test_sslp_oracle_model_matches_creator():
+    for nm in ["Scenario2", "Scenario9"]:
+        m = sslp.scenario_creator(nm, data_dir="x/sslp_15_45_5/scenariodata")
+        sf = m.standard_form()
+        o = om.sslp(nm, instance=5)
+        A = np.zeros((len(sf["bl"]), len(sf["c"])))
+        for i in range(len(sf["bl"])):
+            for k in range(sf["rowptr"][i], sf["rowptr"][i + 1]):
+                A[i, sf["colidx"][k]] = sf["vals"][k]
+        assert np.array_equal(A, o.A) and np.array_equal(sf["c"], o.c)
+        assert np.array_equal(sf["bl"], o.bl) and np.array_equal(sf["bu"], o.bu)
+        assert np.array_equal(sf["lb"], o.lb) and np.array_equal(sf["ub"], o.ub)
+
+
+def check_sslp_ph(lib, device, iters=3):
+    names = sslp.scenario_names_creator(5)
+    ph, conv, Eobj, tb = run_engine(sslp.scenario_creator, names, {"instance": 5}, iters, lib=lib, device=device,
+                                    options={"per_scenario_models": True})
+    o = oph.OraclePH([om.sslp(nm, instance=5) for nm in names], rho=1.0)
+    oc, oE, otb = o.ph_main(iters)
+    # Iter0 LPs may be degenerate (several optimal vertices):
+    # compare the bound at Iter0; from iteration 1 the nonants are unique
+    assert rel(tb, otb) < 1e-8
+    assert rel(ph.xbar_by_node()["ROOT"][0], o.xbar[0]) < 1e-5
+    assert all(s["not_optimal"] == 0 for s in ph.solve_stats)
+    return ph, o
+
+
+def test_sslp_ph_emu(emu):
+    check_sslp_ph(emu, "cpu", iters=2)
