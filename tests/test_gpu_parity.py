@@ -204,3 +204,20 @@ def test_sslp_synthetic_batch_gpu(gpu_lib):
     assert all(s["not_optimal"] == 0 for s in ph.solve_stats)
     o = oph.OraclePH([om.sslp(nm) for nm in names], rho=1.0)
     assert rel(tb, o.iter0()) < 1e-8
+
+
+def test_aircond_bf10x10x10_gpu(gpu_lib):
+    """configs[3]: aircond branching 10x10x10 (1,000 scenarios, 111 non-leaf nodes,
+    per-node x-bar reductions) through the device-driven loop, vs the oracle."""
+    from mpisppy_amd.utils import sputils
+    bfs = [10, 10, 10]
+    names = ["scen%d" % i for i in range(1000)]
+    ph, conv, Eobj, tb = run_engine(aircond.scenario_creator, names, {"branching_factors": bfs}, 3, lib=gpu_lib,
+                                    all_nodenames=sputils.create_nodenames_from_branching_factors(bfs))
+    assert hasattr(ph, "iterk_stats")
+    o = oph.OraclePH([om.aircond(n, bfs) for n in names], rho=1.0)
+    oc, oE, otb = o.ph_main(3)
+    assert rel(tb, otb) < 1e-9
+    assert rel(Eobj, oE) < 1e-8
+    assert rel(ph.W_array(), o.W) < 1e-6
+    assert len(ph.xbar_by_node()) == 111
