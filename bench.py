@@ -60,6 +60,9 @@ def parse():
     ap.add_argument("--cpu-procs", type=int, default=16, help="worker processes (the GPU box's CPU share)")
     ap.add_argument("--host-loop", action="store_true", help="drive each PH iteration from Python")
     ap.add_argument("--depth", type=int, default=4, help="phx_iterk: iterations kept enqueued ahead")
+    ap.add_argument("--fused", type=int, default=1,
+                    help="phx_iterk: one phx_lane_warm launch per PH iteration (Update_W + conv + solve + "
+                         "next x-bar partials fused); 0: k_xbar, k_update_w_seg, warm, cold per iteration")
     ap.add_argument("--timing-every", type=int, default=5,
                     help="phx_iterk: HIP events around the lane kernel of every T-th iteration")
     ap.add_argument("--conv", action="store_true", help="also measure time to conv < 1e-4")
@@ -67,7 +70,7 @@ def parse():
     return ap.parse_args()
 
 
-def lane_bytes(b):
+def lane_bytes(b, fused=False):
     """Algorithmic HBM bytes of phx_lane_warm per scenario.
 
     reads : varying A values, W and rho of the nonant slots with their x-bar
@@ -76,11 +79,16 @@ def lane_bytes(b):
     writes: x (n), row duals y (m), objective, status + iteration count
             (caller's and the context's), flags, active-set words
     The scenario-invariant data are literals of the JIT-specialised kernel.
+    fused (phx_iterk fused mode): + the previous solve's nonant x and the
+    prob_coeff (Update_W / next x-bar partials), + the W write-back.
     """
     nw = (2 * (b.n + b.m) + 31) // 32
     rd = 8 * (b.nvar + 2 * b.nonant.N) + 4 * b.nonant.N + 4 * nw
     rd += 8 * b.n * int(b.c_vary) + 16 * b.n * int(b.bnd_vary) + 16 * b.m * int(b.rhs_vary)
     wr = 8 * (b.n + b.m + 1) + 4 * 5 + 4 * nw
+    if fused:
+        rd += 16 * b.nonant.N
+        wr += 8 * b.nonant.N
     return rd + wr
 
 
@@ -136,7 +144,7 @@ def main():
     S = args.scens
     names = farmer.scenario_names_creator(S)
     solver_opts = {"pdhg_check_every": args.check_every, "lane_solver": args.lane_solver,
-                   "iterk_depth": args.depth, "iterk_timing": args.timing_every}
+                   "iterk_depth": args.depth, "iterk_timing": args.timing_every, "iterk_fused": args.fused}
     if args.ipm_after is not None:
         solver_opts["ipm_after"] = args.ipm_after
     if args.as_rounds is not None:
@@ -184,6 +192,7 @@ def main():
         lane_warm_ms = sum(s.get("lane_warm_ms", 0.0) for s in stats)
         warm_launches = sum(1 for s in stats if s.get("lane_warm_ms", 0.0) > 0.0)
         loop_info = {"loop": "host (PHBase methods per iteration, deferred solves)"}
+        fused_ran = False
     else:
         # PHBase.iterk_loop itself: with no per-iteration hooks it runs on the
         # device (phx_iterk: pipelined iterations, device-side stop test)
@@ -204,7 +213,9 @@ def main():
         stats = []
         lane_warm_ms = st["lane_warm_ms"]
         warm_launches = st["warm_launches"]
-        loop_info = {"loop": "PHBase.iterk_loop -> phx_iterk (device-driven, depth %d)" % args.depth,
+        fused_ran = bool(st.get("fused", False))
+        loop_info = {"loop": "PHBase.iterk_loop -> phx_iterk (device-driven, depth %d%s)"
+                             % (args.depth, ", fused: one launch per PH iteration" if fused_ran else ""),
                      "straggler_stops": st["straggler_stops"], "stragglers": st["stragglers"],
                      "not_optimal": st["not_optimal"]}
     dt_t = torch.tensor([dt], dtype=torch.float64, device="cuda")
@@ -215,7 +226,7 @@ def main():
         # dominant kernel: the warm active-set lane kernel, one launch per step over all local scenarios
         k_ms = lane_warm_ms
         launches = warm_launches
-        bpu = lane_bytes(b)
+        bpu = lane_bytes(b, fused=fused_ran)
         units_per_launch = b.S
         kernel = "phx_lane_warm"
     else:

@@ -278,6 +278,9 @@ typedef struct phx_iterk_args {
                                         time, so the sample is sparse); 0: none            */
     phx_allreduce_fn allreduce;      /* NULL on one rank                         */
     void* allreduce_user;
+    int32_t node_stage_len;          /* doubles in node_stage; >= 2*NNS+1+conv_R enables the
+                                        fused mode (one launch per PH iteration, two-stage
+                                        trees): the all-reduce then carries the conv sums too */
 } phx_iterk_args;
 
 typedef struct phx_iterk_result {
@@ -291,6 +294,7 @@ typedef struct phx_iterk_result {
     double warm_ms;        /* sum of phx_lane_warm durations (timing = 1)       */
     int32_t warm_launches;
     double wall_ms;
+    int32_t fused;         /* 1: the fused one-launch-per-iteration mode ran     */
 } phx_iterk_result;
 
 int phx_iterk(phx_ctx* ctx, const phx_solve_opts* opts, const phx_iterk_args* args,

@@ -197,11 +197,23 @@ inline std::string lane_kernel_source(const LaneStructure& L, int warm_waves = 1
     o << "extern \"C\" __global__ void __launch_bounds__(64, " << warm_waves
       << ") phx_lane_warm(phx_lane::LaneIO io) {\n"
          "  if (phx_lane::gated(io.gate)) return;\n"
+         "  if (io.fz.on && !phx_lane::fz_prologue(io)) return;\n"
          "  phx_lane::zero_next_counts(io.counts_next);\n"
          "  const int t = blockIdx.x * 64 + threadIdx.x;\n"
          "  bool still = false;\n"
-         "  if (t < io.S) still = phx_lane::warm_lane<PT>(io, t);\n"
+         "  double dl = 0.0;\n"
+         "  if (t < io.S) {\n"
+         "    if (io.fz.on) dl = phx_lane::fz_update_w<PT>(io, t);\n"
+         "    still = phx_lane::warm_lane<PT>(io, t);\n"
+         "  }\n"
          "  phx_lane::compact_lane(still, t, io.lanes_out, io.count_out);\n"
+         "  if (io.fz.on) phx_lane::fz_epilogue<PT>(io, t, still, dl);\n"
+         "}\n";
+    // phx_iterk fused mode, after the last enqueued iteration: the decision on
+    // its conv (the next warm launch's prologue does it otherwise)
+    o << "extern \"C\" __global__ void __launch_bounds__(64) phx_fz_tail(phx_lane::LaneIO io) {\n"
+         "  if (phx_lane::gated(io.gate)) return;\n"
+         "  (void)phx_lane::fz_decide(io.fz, io.fz.iter);\n"
          "}\n";
     o << "extern \"C\" __global__ void __launch_bounds__(64, 4) phx_lane_map(phx_lane::LaneIO io) {\n"
          "  if (phx_lane::gated(io.gate)) return;\n"

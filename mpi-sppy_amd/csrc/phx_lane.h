@@ -95,6 +95,43 @@ constexpr int32_t FLAG_IPM_TRIED = 1;   // interior point already attempted
 constexpr int32_t FLAG_WRITTEN = 2;     // outputs written by a lane kernel
 constexpr int32_t FLAG_MAP = 4;         // the lane's affine map (LaneIO::map) matches its stored active set
 
+// phx_iterk's progress word in mapped host memory, polled by the host.
+struct IterkProgress {
+    uint64_t word;   // (iteration << 8) | stop (0 running, 1 converged, 2 generic-path lanes):
+                     // one 8-byte store, so the host never sees a torn pair
+    double conv;     // read by the host only after the stream drained
+};
+
+// phx_iterk, fused mode (two-stage trees): ONE launch of phx_lane_warm is a
+// whole PH iteration k.  Per lane: Update_W (W += rho (x_{k-1} - x-bar_k),
+// phbase.py:293-318) and |x_{k-1} - x-bar_k| (convergence_diff,
+// phbase.py:321-343), then solve k with the new W; the lane's
+// prob_coeff-weighted x and x^2 of solve k are the partial sums of iteration
+// k+1's Compute_Xbar (phbase.py:54-80).  Per-block partials are folded by the
+// last block of each arrival shard, then by the last shard, into the stage
+// buffer of iteration k+1.  The stop test on conv_k runs in the prologue of
+// the NEXT launch (after the all-reduce on several ranks), so solve k is
+// speculative: it writes the other output buffer set and is simply not
+// committed when conv_k < convthresh.
+struct FusedW {
+    int32_t on;
+    int32_t iter;              // k
+    int32_t first;             // first iteration of a pipeline segment: no decision on conv_{k-1}
+    double* stage;             // [2*nns sums | straggler count | R conv sums]: read as iteration k's,
+                               // overwritten by the last block with iteration k+1's
+    double* node_sums;         // published x-bar | xsqbar (block 0, once the iteration proceeds)
+    int32_t nns;               // node-slot count (= nonant slots: one tree node)
+    const double* x_prev;      // solve k-1's x [n][S]
+    const double* pc;          // prob_coeff [N][S]
+    int32_t* ctl;              // [0] stop flag (the gate of later kernels), [1] stop iteration
+    IterkProgress* prog;
+    double* part;              // [gridDim.x * NV] block partials, then [TICKET_SHARDS * NV] shard partials
+    unsigned int* tk;          // sharded arrival counters (TICKET_SET words)
+    int32_t g, R;              // this rank's emulated-rank entry, emulated rank count
+    const double* cnt;         // [R] element counts (convergence_diff's denominators)
+    double thresh;
+};
+
 // Runtime inputs/outputs (device pointers; per-scenario arrays [i*S + s]).
 // A, c, bounds below are scaled iff PT::scaled() (phx_jit.h LaneStructure).
 struct LaneIO {
@@ -141,6 +178,7 @@ struct LaneIO {
     int32_t warm_rounds;   // active-set rounds per warm pass
     const int32_t* gate;   // *gate != 0: the launch does nothing (phx_iterk past its stop), or null
     double* map;           // [map_words<PT>()][S] affine solution maps (see map_apply), or null
+    FusedW fz;             // phx_iterk fused Update_W (fz.on = 0 otherwise)
 };
 
 // phx_iterk gate: every kernel of an iteration past the device-side stop exits
@@ -1064,6 +1102,198 @@ PHX_LD bool cold_lane(const LaneIO& io, int sc) {
 }
 
 #if defined(__HIPCC__) || defined(__HIPCC_RTC__)
+// Inter-workgroup hand-off of the per-block partials without fences
+// (MI355X_MICROARCH.md, inter-workgroup visibility: write-through `sc1`
+// payload stores, drained, then one agent-scope atomic per workgroup; the
+// workgroup whose add returns last reads with `sc1` loads after a barrier).
+// An agent release would write back the XCD L2 — the W stores of
+// k_update_w_seg included, several us — and the acquire invalidate L1.
+__device__ __forceinline__ void store_wt(double* p, double v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double load_wt(const double* p) {
+    return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Returns true (block-uniform) in the block that arrives last.  The partials
+// must have been stored with store_wt by thread 0 (the thread that adds).
+// Arrivals are sharded over TICKET_SHARDS counters on lines of their own (one
+// counter serialises its atomics at ~12 ns each: 391 arrivals on one word cost
+// ~5 us); the last arriver of each shard adds to the top counter, whose last
+// arriver is the last block overall.  The last block resets every counter.
+#define TICKET_SHARDS 8
+#define TICKET_STRIDE 32                        // 128-B lines
+#define TICKET_SET ((TICKET_SHARDS + 1) * TICKET_STRIDE)
+__device__ bool arrive_last(unsigned int* tk, unsigned int nblocks) {
+    __shared__ unsigned int s_last;
+    if (threadIdx.x == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned b = blockIdx.x, k = b % TICKET_SHARDS;
+        const unsigned nk = (nblocks - k + TICKET_SHARDS - 1) / TICKET_SHARDS;   // blocks of shard k
+        const unsigned nsh = nblocks < TICKET_SHARDS ? nblocks : TICKET_SHARDS;   // non-empty shards
+        unsigned last = 0;
+        if (__hip_atomic_fetch_add(tk + k * TICKET_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+            nk - 1u)
+            last = __hip_atomic_fetch_add(tk + TICKET_SHARDS * TICKET_STRIDE, 1u, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT) == nsh - 1u;
+        if (last)
+            for (int q = 0; q <= TICKET_SHARDS; ++q) tk[q * TICKET_STRIDE] = 0u;
+        s_last = last;
+    }
+    __syncthreads();
+    return s_last != 0u;
+}
+
+__device__ __forceinline__ void publish_progress(IterkProgress* p, int iter, int done, double conv) {
+    // relaxed system-scope stores: no fence (a system release would write back
+    // and invalidate the L2); the host orders nothing else on this word
+    __hip_atomic_store(&p->conv, conv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&p->word, ((uint64_t)(uint32_t)iter << 8) | (uint64_t)done, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// conv_{it} from the stage buffer (phbase.py:330-343: mean over emulated ranks
+// of each rank's mean |x - x-bar|, ranks in order); the stop test
+// (phbase.py:914-926).  Uniform over the grid: every block reads the same
+// numbers.  Block 0 publishes the decision.  true: stopped.
+__device__ __forceinline__ bool fz_decide(const FusedW& f, int it) {
+    const double* seg = f.stage + 2 * f.nns + 1;
+    double tot = 0.0;
+    for (int r = 0; r < f.R; ++r)
+        if (f.cnt[r] > 0) tot += seg[r] / f.cnt[r];
+    const double conv = tot / f.R;
+    const bool done = conv < f.thresh;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (done) {
+            f.ctl[1] = it;
+            *(volatile int32_t*)f.ctl = 1;
+        }
+        publish_progress(f.prog, it, done ? 1 : 0, conv);
+    }
+    return done;
+}
+
+// Prologue (block-uniform; before anything is written): the decision on
+// conv_{k-1}; then a previous solve that left lanes to the generic path stops
+// the pipeline at k (every rank sees the same all-reduced count) before W is
+// touched.  Block 0 publishes x-bar_k.
+__device__ bool fz_prologue(const LaneIO& io) {
+    const FusedW& f = io.fz;
+    if (!f.first && fz_decide(f, f.iter - 1)) return false;
+    if (f.stage[2 * f.nns] > 0.5) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            f.ctl[1] = f.iter;
+            *(volatile int32_t*)f.ctl = 2;
+            publish_progress(f.prog, f.iter, 2, 0.0);
+        }
+        return false;
+    }
+    if (blockIdx.x == 0)
+        for (int e = threadIdx.x; e < 2 * f.nns; e += blockDim.x) f.node_sums[e] = f.stage[e];
+    return true;
+}
+
+// Update_W for one lane (in place, before its Data reads W): returns the
+// lane's sum |x_{k-1} - x-bar_k| over its nonant slots.
+template <class PT>
+__device__ double fz_update_w(const LaneIO& io, int sc) {
+    const FusedW& f = io.fz;
+    const int64_t S = io.S;
+    double d = 0.0;
+    PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
+        const int t = PT::col_slot(j);
+        if (t >= 0) {
+            const int64_t o = (int64_t)t * S + sc;
+            const double diff = f.x_prev[(int64_t)j * S + sc] - f.stage[io.xbar_idx[o]];
+            const_cast<double*>(io.W)[o] = io.W[o] + io.rho[o] * diff;
+            d += fabs(diff);
+        }
+    }
+    return d;
+}
+
+// Epilogue: the block's partials [sum pc x | sum pc x^2 per slot | sum |d|]
+// (one wavefront: shuffles), stored write-through; the last block of each
+// arrival shard folds its shard's blocks (shard = blockIdx % 8, which is the
+// XCD the block ran on), the last shard's folder folds the shards and writes
+// the stage buffer of iteration k+1 (+ the straggler count of solve k and
+// this rank's conv sum).  Fixed order: independent of arrival order.
+template <class PT>
+__device__ void fz_epilogue(const LaneIO& io, int sc, bool still, double dl) {
+    const FusedW& f = io.fz;
+    constexpr int NS = PT::nslot() > 0 ? PT::nslot() : 1;
+    constexpr int NV = 2 * NS + 1;
+    const int64_t S = io.S;
+    double v[NV];
+    PHX_UNROLL for (int e = 0; e < NV; ++e) v[e] = 0.0;
+    if (sc < io.S) {
+        v[2 * NS] = dl;
+        if (!still)
+            PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
+                const int t = PT::col_slot(j);
+                if (t >= 0) {
+                    const double xu = io.x_out[(int64_t)j * S + sc];
+                    const double w = f.pc[(int64_t)t * S + sc] * xu;
+                    v[t] += w;
+                    v[NS + t] += w * xu;
+                }
+            }
+    }
+    PHX_UNROLL for (int e = 0; e < NV; ++e)
+        for (int off = 32; off > 0; off >>= 1) v[e] += __shfl_down(v[e], off, 64);
+    const unsigned nb = gridDim.x, b = blockIdx.x, k = b % TICKET_SHARDS;
+    const unsigned nk = (nb - k + TICKET_SHARDS - 1) / TICKET_SHARDS;
+    const unsigned nsh = nb < TICKET_SHARDS ? nb : TICKET_SHARDS;
+    double* shard_part = f.part + (int64_t)nb * NV;
+    __shared__ unsigned s_state;
+    if (threadIdx.x == 0) {
+        PHX_UNROLL for (int e = 0; e < NV; ++e) store_wt(&f.part[(int64_t)b * NV + e], v[e]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        s_state = __hip_atomic_fetch_add(f.tk + k * TICKET_STRIDE, 1u, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT) == nk - 1u;
+    }
+    __syncthreads();
+    if (!s_state) return;
+    // last of shard k: blocks k, k+8, ... in order (4 blocks' loads in flight)
+    PHX_UNROLL for (int e = 0; e < NV; ++e) v[e] = 0.0;
+    for (unsigned i0 = threadIdx.x; i0 < nk; i0 += 4 * 64) {
+        double l[4][NV];
+        PHX_UNROLL for (int u = 0; u < 4; ++u) {
+            const unsigned i = i0 + 64u * u;
+            PHX_UNROLL for (int e = 0; e < NV; ++e)
+                l[u][e] = i < nk ? load_wt(&f.part[(int64_t)(k + TICKET_SHARDS * i) * NV + e]) : 0.0;
+        }
+        PHX_UNROLL for (int u = 0; u < 4; ++u) PHX_UNROLL for (int e = 0; e < NV; ++e) v[e] += l[u][e];
+    }
+    PHX_UNROLL for (int e = 0; e < NV; ++e)
+        for (int off = 32; off > 0; off >>= 1) v[e] += __shfl_down(v[e], off, 64);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        PHX_UNROLL for (int e = 0; e < NV; ++e) store_wt(&shard_part[k * NV + e], v[e]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const bool last = __hip_atomic_fetch_add(f.tk + TICKET_SHARDS * TICKET_STRIDE, 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT) == nsh - 1u;
+        if (last)
+            for (int q = 0; q <= TICKET_SHARDS; ++q) f.tk[q * TICKET_STRIDE] = 0u;
+        s_state = last ? 2u : 0u;
+    }
+    __syncthreads();
+    if (s_state != 2u) return;
+    // the last block overall: shards in order, then iteration k+1's stage
+    const int e = threadIdx.x;
+    if (e < NV) {
+        double a = 0.0;
+        for (unsigned q = 0; q < nsh; ++q) a += load_wt(&shard_part[q * NV + e]);
+        if (e < NS) f.stage[e] = a;
+        else if (e < 2 * NS) f.stage[f.nns + (e - NS)] = a;
+        else {
+            for (int r = 0; r < f.R; ++r) f.stage[2 * f.nns + 1 + r] = r == f.g ? a : 0.0;
+            f.stage[2 * f.nns] =
+                (double)__hip_atomic_load(io.count_out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
 // Compact the lanes that still need work into out[0..*count): one atomic per
 // wavefront, lane order kept within the wavefront.  Every lane of the
 // wavefront must reach this call.

@@ -419,6 +419,9 @@ class PHBase(SPOpt):
         a.max_iters = int(max_iterations)
         a.depth = int(so_dict.get("iterk_depth", 4))
         a.timing = int(so_dict.get("iterk_timing", 0))
+        # fused mode (one launch per PH iteration, two-stage trees) unless
+        # {"iterk_fused": 0}; the library decides whether the problem allows it
+        a.node_stage_len = self._node_stage.numel() if int(so_dict.get("iterk_fused", 1)) else 0
         res = _native.IterkResult()
         t0 = time.perf_counter()
         lib.check(self._ctx, lib.iterk(self._ctx, ctypes.byref(so), ctypes.byref(a), ctypes.byref(res),
@@ -434,7 +437,8 @@ class PHBase(SPOpt):
         self.iterk_stats = {"iters": int(res.iters), "converged": bool(res.converged), "solves": int(res.solves),
                             "straggler_stops": int(res.straggler_stops), "stragglers": int(res.stragglers),
                             "not_optimal": int(res.not_optimal), "lane_warm_ms": float(res.warm_ms),
-                            "warm_launches": int(res.warm_launches), "wall_s": wall}
+                            "warm_launches": int(res.warm_launches), "wall_s": wall,
+                            "fused": bool(res.fused)}
         if res.not_optimal:
             stc = self._status.cpu().numpy()
             name = self.__class__.__name__

@@ -312,9 +312,10 @@ class SPBase:
         NNS1 = max(self.NNS, 1)
         self._xbar_node = self._node_buf[:NNS1]
         self._xsqbar_node = self._node_buf[NNS1:2 * NNS1]
-        # phx_iterk: this iteration's sums (+ the straggler count), all-reduced
-        # before they are published into _node_buf
-        self._node_stage = torch.zeros(2 * NNS1 + 1, dtype=f64, device=self.device)
+        # phx_iterk: this iteration's sums (+ the straggler count, + the
+        # per-emulated-rank conv sums in the fused mode), all-reduced before
+        # they are published into _node_buf
+        self._node_stage = torch.zeros(2 * NNS1 + 1 + self._conv_R, dtype=f64, device=self.device)
         self._dsum = torch.zeros(S, dtype=f64, device=self.device)
         # per-emulated-rank |x - xbar| sums + one slot for the straggler count of
         # a deferred solve (all-reduced together, phbase.convergence_diff)

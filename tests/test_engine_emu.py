@@ -166,10 +166,14 @@ def test_native_loop_matches_host_loop_emu(emu, case):
     check_native_vs_host(emu, "cpu", case)
 
 
-def check_native_vs_host(lib, device, case, S=30, solver=None):
+def check_native_vs_host(lib, device, case, S=30, solver=None, fused=0):
+    """fused=0: bit for bit.  fused=1 (GPU): phx_iterk's one-launch-per-iteration
+    mode sums x-bar and conv in another fixed order, so they agree to 1e-9."""
     runs = []
     for nl in (1, 0):
         so = dict(solver or {}, native_loop=nl)
+        if nl:
+            so["iterk_fused"] = fused
         opts = {"iter0_solver_options": dict(solver or {}), "iterk_solver_options": so}
         kw = dict(lib=lib, device=device, options=opts)
         if case == "aircond":
@@ -192,6 +196,19 @@ def check_native_vs_host(lib, device, case, S=30, solver=None):
     assert a._PHIter == b._PHIter
     if case == "converge":
         assert a.iterk_stats["converged"] and a._PHIter < 400
+    if fused:
+        assert a.iterk_stats["fused"] == (case in ("farmer", "converge"))
+        if a.iterk_stats["fused"]:
+            def rel(u, v):
+                u, v = np.asarray(u, dtype=float), np.asarray(v, dtype=float)
+                return float(np.max(np.abs(u - v) / np.maximum(1.0, np.abs(v)))) if u.size else 0.0
+            assert rel(a.W_array(), b.W_array()) < 1e-9
+            assert rel(a.nonant_values(), b.nonant_values()) < 1e-9
+            for k, v in b.xbar_by_node().items():
+                assert rel(a.xbar_by_node()[k][0], v[0]) < 1e-9
+            assert rel(ca, cb) < 1e-9 and rel(Ea, Eb) < 1e-9 and ta == tb_
+            return a, b
+    assert not a.iterk_stats.get("fused", False)
     assert np.array_equal(a.W_array(), b.W_array())
     assert np.array_equal(a.nonant_values(), b.nonant_values())
     for k, v in b.xbar_by_node().items():

@@ -157,12 +157,22 @@ def test_native_loop_matches_host_loop_gpu(gpu_lib, case):
     check_native_vs_host(gpu_lib, None, case, S=1000)
 
 
-@pytest.mark.parametrize("so", [{"as_rounds": 0, "ipm_max_it": 2}, {"as_rounds": 1, "ipm_max_it": 3}])
-def test_native_loop_straggler_stops_gpu(gpu_lib, so):
+@pytest.mark.parametrize("case", ["farmer", "aircond", "conv_ranks", "converge"])
+def test_native_loop_fused_matches_host_loop_gpu(gpu_lib, case):
+    """phx_iterk fused mode (one phx_lane_warm launch per PH iteration: Update_W,
+    conv partials, solve, next x-bar partials) == the Python loop to 1e-9, same
+    iteration count; multistage / emulated-rank cases fall back (bit for bit)."""
+    from test_engine_emu import check_native_vs_host
+    check_native_vs_host(gpu_lib, None, case, S=1000, fused=1)
+
+
+@pytest.mark.parametrize("so,fused", [({"as_rounds": 0, "ipm_max_it": 2}, 0), ({"as_rounds": 1, "ipm_max_it": 3}, 0),
+                                      ({"as_rounds": 1, "ipm_max_it": 3}, 1)])
+def test_native_loop_straggler_stops_gpu(gpu_lib, so, fused):
     """Starved lane solves leave lanes to the generic path: phx_iterk stops the
     pipeline, finishes them and resumes; the trajectory equals the host loop's."""
     from test_engine_emu import check_native_vs_host
-    a, b = check_native_vs_host(gpu_lib, None, "farmer", S=2000, solver=so)
+    a, b = check_native_vs_host(gpu_lib, None, "farmer", S=2000, solver=so, fused=fused)
     assert a.iterk_stats["straggler_stops"] > 0
 
 
