@@ -99,6 +99,13 @@ def pdhg_bytes(b):
     return 8 * (2 * b.nvar + 2 * b.n + 2 * b.m) + 8 * (7 * b.n + 5 * b.m)
 
 
+def wg_bytes(b):
+    """Algorithmic bytes of one scenario solve in k_wg_warm (phx_wg.h): reads
+    the varying A values, qN/pN of the nonant slots and the warm-start point
+    (x n, y m); writes x, x0, xT (3n) and y, y0, yT (3m) plus status + iters."""
+    return 8 * (b.nvar + 2 * b.nonant.N + b.n + b.m) + 8 * (3 * b.n + 3 * b.m) + 8
+
+
 def pmc_traffic(kernel, args):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
     (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; scripts/pmc_summary.py).
@@ -229,6 +236,13 @@ def main():
         bpu = lane_bytes(b, fused=fused_ran)
         units_per_launch = b.S
         kernel = "phx_lane_warm"
+    elif sum(s.get("wg_ms", 0.0) for s in stats) > 0.0:
+        # generic path with the workgroup warm active-set pass (medium subproblems)
+        k_ms = sum(s.get("wg_ms", 0.0) for s in stats)
+        launches = sum(1 for s in stats if s.get("wg_ms", 0.0) > 0.0)
+        bpu = wg_bytes(b)
+        units_per_launch = b.S
+        kernel = "k_wg_warm"
     else:
         k_ms = sum(s["pdhg_ms"] for s in stats)
         launches = sum(s["launches"] for s in stats)
@@ -261,7 +275,7 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/launch",
                      "traffic_source": traffic_src, "algorithmic_bytes_per_launch": bytes_per_launch,
                      "kernel": kernel, "bytes_per_unit": bpu,
-                     "unit_def": "scenario solve" if lane_on else "scenario PDHG iteration",
+                     "unit_def": "scenario PDHG iteration" if kernel == "k_chunk" else "scenario solve",
                      "units_per_launch": units_per_launch,
                      "avg_launch_us": avg_launch_s * 1e6, "launches": launches},
         "loop": loop_info,
@@ -271,7 +285,9 @@ def main():
                                "lane_cold": sum(s.get("lane_ms", 0.0) for s in stats) / K,
                                "pdhg": sum(s["pdhg_ms"] for s in stats) / K,
                                "polish": sum(s["polish_ms"] for s in stats) / K,
-                               "ipm": sum(s["ipm_ms"] for s in stats) / K},
+                               "ipm": sum(s["ipm_ms"] for s in stats) / K,
+                               "wg_warm": sum(s.get("wg_ms", 0.0) for s in stats) / K},
+        "wg_certified_per_step": [s.get("wg_certified") for s in stats],
         "lane_certified_per_step": [s.get("lane_certified") for s in stats],
         "lane_warm_certified_per_step": [s.get("lane_warm_certified") for s in stats],
         "lane_first_certified_per_step": [s.get("lane_first_certified") for s in stats],

@@ -94,6 +94,12 @@ typedef struct phx_solve_opts {
                                  host synchronisation); phx_solve_finish then
                                  completes the solve (generic path for the
                                  lanes the lane solver could not certify)     */
+    int32_t wg_warm;          /* k > 0: a warm generic-path solve (subproblems
+                                 above the lane limits) first runs the
+                                 workgroup-per-scenario active-set KKT pass,
+                                 up to k rounds from the previous solution;
+                                 PDHG + polish only for the lanes it does not
+                                 certify.  0: off                             */
 } phx_solve_opts;
 
 /* Statistics of the most recent phx_solve (HIP events on the solve stream). */
@@ -116,6 +122,8 @@ typedef struct phx_solve_stats {
     int32_t jit;              /* 1 if this context has a specialised kernel   */
     int32_t lane_first_certified; /* certified by the first lane pass (the
                                  affine-map pass when maps are on)            */
+    int32_t wg_certified;     /* certified by the workgroup warm pass         */
+    double  wg_ms;            /* workgroup warm pass kernel time              */
 } phx_solve_stats;
 
 /* Scenario-tree reduction layout for Compute_Xbar (phbase.py:27-107): for each

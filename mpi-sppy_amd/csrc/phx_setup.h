@@ -111,4 +111,33 @@ inline void build_seg_tiles(const std::vector<int32_t>& s0, const std::vector<in
     }
 }
 
+// Schur-complement pair list of the workgroup solver (phx_wg.h WgPairs):
+// every (ia >= ib) row pair sharing a column, with the CSR positions of the
+// shared column in both rows, in (ia, ib) order.  Built from the CSC view.
+struct WgPairsHost {
+    std::vector<int32_t> ptr, ia, ib, ka, kb;
+};
+
+inline void build_wg_pairs(const HostSetup& hs, int n, int m, WgPairsHost& out) {
+    std::vector<std::vector<std::pair<int32_t, int32_t>>> trip((size_t)m * m);
+    for (int j = 0; j < n; ++j)
+        for (int a = hs.colptr[j]; a < hs.colptr[j + 1]; ++a)
+            for (int b = hs.colptr[j]; b < hs.colptr[j + 1]; ++b) {
+                const int ra = hs.rowidx[a], rb = hs.rowidx[b];
+                if (ra < rb) continue;
+                trip[(size_t)ra * m + rb].push_back({hs.csc2csr[a], hs.csc2csr[b]});
+            }
+    out = WgPairsHost{};
+    out.ptr.push_back(0);
+    for (int ia = 0; ia < m; ++ia)
+        for (int ib = 0; ib <= ia; ++ib) {
+            const auto& t = trip[(size_t)ia * m + ib];
+            if (t.empty()) continue;
+            out.ia.push_back(ia);
+            out.ib.push_back(ib);
+            for (const auto& pr : t) { out.ka.push_back(pr.first); out.kb.push_back(pr.second); }
+            out.ptr.push_back((int32_t)out.ka.size());
+        }
+}
+
 }  // namespace phx

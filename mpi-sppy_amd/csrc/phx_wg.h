@@ -1,0 +1,322 @@
+// phx_wg.h — workgroup-per-scenario warm active-set KKT solve for medium
+// subproblems (farmer crops_multiplier=10, sslp relaxations: n in the
+// hundreds, m <= ~100), the generic-path counterpart of phx_lane_warm.
+//
+// Reference semantics being replaced: SPOpt.solve_one (mpisppy/spopt.py:85-223)
+// of PH iterations >= 1 (phbase.py:875-979): the external solver warm-starts
+// from its previous basis.  Here one 64-lane wavefront owns one scenario: its
+// A values, costs, iterate and the dense Schur complement of the active rows
+// live in LDS, and every phase is a wavefront-strided loop over columns, rows
+// or Schur entries separated by a workgroup barrier (a single wave: the
+// barrier only orders LDS).  Starting from the previous solve's point
+// (St.xT/yT, scaled) it runs up to `rounds` rounds of
+//   classify -> Schur A_RF (P_FF+reg)^-1 A_RF' + reg I -> Cholesky ->
+//   iterative refinement on the unregularised KKT -> certificate ->
+//   primal-dual active-set update,
+// with exactly the classification, refinement and certificate of polish_lane
+// (phx_core.h), so a certified lane is as exact as a polished PDHG lane.
+// Lanes that do not certify go to the PDHG + polish path unchanged.
+//
+// The same code is compiled for the host by tests/emu with WG_NT = 1 (every
+// strided loop runs serially, barriers vanish): each phase writes only
+// elements it owns, and cross-thread values are exchanged only through LDS
+// across a barrier, so the serial run computes the same numbers.
+#pragma once
+#include "phx_core.h"
+
+namespace phx {
+
+#if defined(__HIP_DEVICE_COMPILE__)
+#define WG_TID ((int)threadIdx.x)
+#define WG_NT 64
+#define WG_SYNC() __syncthreads()
+#else
+#define WG_TID 0
+#define WG_NT 1
+#define WG_SYNC() ((void)0)
+#endif
+
+// Schur-complement entries (ia >= ib) whose rows share a column, with the CSR
+// positions (ka in row ia, kb in row ib) of every shared column, built once on
+// the host from the pattern (phx_set_problem).
+struct WgPairs {
+    int32_t npair;
+    const int32_t* ptr;   // [npair+1] into ka/kb
+    const int32_t* ia;    // [npair]
+    const int32_t* ib;    // [npair]
+    const int32_t* ka;    // [ntrip]
+    const int32_t* kb;    // [ntrip]
+};
+
+// Carve of the dynamic LDS of one scenario.
+struct WgLds {
+    double *Sm, *dg, *a, *xp, *r1, *qq, *pp, *z, *t, *u;
+    int32_t* flag;
+    int8_t *cc, *rc;   // column code 0 free / 1 at l / 2 at u; row code 0 inactive / 1 at bl / 2 at bu
+};
+
+PHX_HD size_t wg_lds_bytes(int n, int m, int nnz) {
+    size_t b = 8 * ((size_t)m * m + 4 * (size_t)m + (size_t)nnz + 4 * (size_t)n) + 16 + (size_t)n + (size_t)m;
+    return (b + 15) & ~(size_t)15;
+}
+
+PHX_HD WgLds wg_carve(void* base, int n, int m, int nnz) {
+    WgLds L;
+    double* d = (double*)base;
+    L.Sm = d; d += (size_t)m * m;
+    L.dg = d; d += m;
+    L.z = d; d += m;
+    L.t = d; d += m;
+    L.u = d; d += m;
+    L.a = d; d += nnz;
+    L.xp = d; d += n;
+    L.r1 = d; d += n;
+    L.qq = d; d += n;
+    L.pp = d; d += n;
+    L.flag = (int32_t*)d;
+    int8_t* c = (int8_t*)(L.flag + 4);
+    L.cc = c; c += n;
+    L.rc = c;
+    return L;
+}
+
+// max over the workgroup (one wavefront: butterfly over its 64 lanes)
+PHX_HD double wg_max(double v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+#endif
+    return v;
+}
+
+// Returns true (uniformly) iff the point in L.xp / L.z passes the KKT
+// certificate; rounds > 1 allow primal-dual active-set updates in between.
+PHX_HD bool wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts& O, int s, const WgLds& L,
+                    int rounds, double tol0) {
+    const int S = P.S, n = P.n, m = P.m;
+    const double reg = O.reg;
+    // ---- scenario data into LDS ----
+    for (int k = WG_TID; k < P.nnz; k += WG_NT) L.a[k] = aval(P, k, s);
+    double qm = 0.0;
+    for (int j = WG_TID; j < n; j += WG_NT) {
+        double q, p;
+        col_cost(P, j, s, q, p);
+        L.qq[j] = q;
+        L.pp[j] = p;
+        qm = fmax(qm, fabs(q / P.dc[j]));
+    }
+    const double dtol = O.kkt_tol * (1.0 + wg_max(qm));
+    const double ptol = O.kkt_tol;
+    WG_SYNC();
+    // ---- round 0: classify the previous solution (polish_lane's rule) ----
+    for (int j = WG_TID; j < n; j += WG_NT) {
+        const int64_t o = ix(j, s, S);
+        const double x = St.xT[o];
+        const double l = P.lb.at(j, s), u = P.ub.at(j, s);
+        double aty = 0.0;
+        for (int k = P.colptr[j]; k < P.colptr[j + 1]; ++k)
+            aty += L.a[P.csc2csr[k]] * St.yT[ix(P.rowidx[k], s, S)];
+        const double lam = L.qq[j] + L.pp[j] * x - aty;
+        int8_t c = 0;
+        if (isfinite(l) && (x - l <= tol0 * (1.0 + fabs(l)) || x - l < lam)) c = 1;
+        else if (isfinite(u) && (u - x <= tol0 * (1.0 + fabs(u)) || u - x < -lam)) c = 2;
+        L.cc[j] = c;
+        L.xp[j] = c == 1 ? l : (c == 2 ? u : x);
+    }
+    for (int i = WG_TID; i < m; i += WG_NT) {
+        double ax = 0.0;
+        for (int k = P.rowptr[i]; k < P.rowptr[i + 1]; ++k) ax += L.a[k] * St.xT[ix(P.colidx[k], s, S)];
+        const double bl = P.bl.at(i, s), bu = P.bu.at(i, s);
+        const double yv = St.yT[ix(i, s, S)];
+        int8_t r = 0;
+        if (isfinite(bl) && (ax - bl <= tol0 * (1.0 + fabs(bl)) || ax - bl < yv)) r = 1;
+        else if (isfinite(bu) && (bu - ax <= tol0 * (1.0 + fabs(bu)) || bu - ax < -yv)) r = 2;
+        L.rc[i] = r;
+        L.z[i] = r ? -yv : 0.0;
+    }
+    WG_SYNC();
+    for (int round = 0; round < rounds; ++round) {
+        if (WG_TID == 0) L.flag[0] = 0;
+        // ---- Schur complement (lower part) ----
+        for (int e = WG_TID; e < m * m; e += WG_NT) {
+            const int i = e / m, k = e - i * m;
+            L.Sm[e] = (i == k) ? (L.rc[i] ? reg : 1.0) : 0.0;
+        }
+        WG_SYNC();
+        for (int p = WG_TID; p < G.npair; p += WG_NT) {
+            const int ia = G.ia[p], ib = G.ib[p];
+            if (!L.rc[ia] || !L.rc[ib]) continue;
+            double v = 0.0;
+            for (int t = G.ptr[p]; t < G.ptr[p + 1]; ++t) {
+                const int ka = G.ka[t], j = P.colidx[ka];
+                if (L.cc[j] == 0) v += L.a[ka] * L.a[G.kb[t]] / (L.pp[j] + reg);
+            }
+            L.Sm[ia * m + ib] += v;
+        }
+        WG_SYNC();
+        // ---- Cholesky: trailing update on the lower part, L[i][k] (i > k)
+        //      stored transposed at Sm[k*m+i], 1/diagonal in dg ----
+        bool spd = true;
+        for (int jj = 0; jj < m; ++jj) {
+            const double d = L.Sm[jj * m + jj];
+            if (!(d > 0.0)) { spd = false; break; }
+            const double sd = sqrt(d), id = 1.0 / d;
+            for (int i = jj + 1 + WG_TID; i < m; i += WG_NT) {
+                double* row = L.Sm + (size_t)i * m;
+                const double lij = row[jj];
+                L.Sm[jj * m + i] = lij / sd;
+                const double f = lij * id;
+                int k = jj + 1;
+                // batches of 4: all loads issued before the stores (LDS
+                // pointers may alias as far as the compiler knows)
+                for (; k + 3 <= i; k += 4) {
+                    const double c0 = L.Sm[k * m + jj], c1 = L.Sm[(k + 1) * m + jj];
+                    const double c2 = L.Sm[(k + 2) * m + jj], c3 = L.Sm[(k + 3) * m + jj];
+                    const double r0 = row[k], r1 = row[k + 1], r2 = row[k + 2], r3 = row[k + 3];
+                    row[k] = r0 - f * c0; row[k + 1] = r1 - f * c1;
+                    row[k + 2] = r2 - f * c2; row[k + 3] = r3 - f * c3;
+                }
+                for (; k <= i; ++k) row[k] -= f * L.Sm[k * m + jj];
+            }
+            if (WG_TID == 0) L.dg[jj] = 1.0 / sd;
+            WG_SYNC();
+        }
+        if (!spd) return false;
+        // ---- explicit inverse of L into the lower part (diagonal included):
+        //      one column per thread, no cross-thread dependence ----
+        for (int c = WG_TID; c < m; c += WG_NT) {
+            L.Sm[c * m + c] = L.dg[c];
+            for (int i = c + 1; i < m; ++i) {
+                double v = 0.0;
+                for (int k = c; k < i; ++k) v += L.Sm[k * m + i] * L.Sm[k * m + c];
+                L.Sm[i * m + c] = -v * L.dg[i];
+            }
+        }
+        WG_SYNC();
+        // ---- iterative refinement on the unregularised KKT ----
+        for (int it = 0; it < O.refine_steps; ++it) {
+            for (int j = WG_TID; j < n; j += WG_NT) {
+                if (L.cc[j]) { L.r1[j] = 0.0; continue; }
+                double atz = 0.0;
+                for (int k = P.colptr[j]; k < P.colptr[j + 1]; ++k) atz += L.a[P.csc2csr[k]] * L.z[P.rowidx[k]];
+                L.r1[j] = -L.qq[j] - L.pp[j] * L.xp[j] - atz;
+            }
+            WG_SYNC();
+            for (int i = WG_TID; i < m; i += WG_NT) {
+                if (!L.rc[i]) { L.t[i] = 0.0; continue; }
+                double adr = 0.0, ax = 0.0;
+                for (int k = P.rowptr[i]; k < P.rowptr[i + 1]; ++k) {
+                    const int j = P.colidx[k];
+                    ax += L.a[k] * L.xp[j];
+                    if (!L.cc[j]) adr += L.a[k] * L.r1[j] / (L.pp[j] + reg);
+                }
+                const double b = L.rc[i] == 1 ? P.bl.at(i, s) : P.bu.at(i, s);
+                L.t[i] = adr - (b - ax);
+            }
+            WG_SYNC();
+            // u = L^-1 t ; then t = L^-T u (dz)
+            for (int i = WG_TID; i < m; i += WG_NT) {
+                double v = 0.0;
+                for (int k = 0; k <= i; ++k) v += L.Sm[i * m + k] * L.t[k];
+                L.u[i] = v;
+            }
+            WG_SYNC();
+            for (int k = WG_TID; k < m; k += WG_NT) {
+                double v = 0.0;
+                for (int i = k; i < m; ++i) v += L.Sm[i * m + k] * L.u[i];
+                L.t[k] = v;
+            }
+            WG_SYNC();
+            for (int j = WG_TID; j < n; j += WG_NT) {
+                if (L.cc[j]) continue;
+                double atz = 0.0;
+                for (int k = P.colptr[j]; k < P.colptr[j + 1]; ++k) atz += L.a[P.csc2csr[k]] * L.t[P.rowidx[k]];
+                L.xp[j] += (L.r1[j] - atz) / (L.pp[j] + reg);
+            }
+            for (int i = WG_TID; i < m; i += WG_NT)
+                if (L.rc[i]) L.z[i] += L.t[i];
+            WG_SYNC();
+        }
+        // ---- certificate (polish_lane's, unscaled quantities); keeps the
+        //      multipliers (r1) and row activities (t) for the update ----
+        bool bad = false;
+        for (int j = WG_TID; j < n; j += WG_NT) {
+            const double x = L.xp[j];
+            const double l = P.lb.at(j, s), u = P.ub.at(j, s);
+            const double dc = P.dc[j];
+            if (x < l && (l - x) * dc > ptol * (1.0 + fabs(l * dc))) bad = true;
+            if (x > u && (x - u) * dc > ptol * (1.0 + fabs(u * dc))) bad = true;
+            double atz = 0.0;
+            for (int k = P.colptr[j]; k < P.colptr[j + 1]; ++k) atz += L.a[P.csc2csr[k]] * L.z[P.rowidx[k]];
+            const double lam = (L.qq[j] + L.pp[j] * x + atz) / dc;
+            L.r1[j] = lam;
+            const int8_t c = L.cc[j];
+            if (c == 0) {
+                if (fabs(lam) > dtol) bad = true;
+            } else if (!(l == u)) {
+                if (c == 1 && lam < -dtol) bad = true;
+                if (c == 2 && lam > dtol) bad = true;
+            }
+        }
+        for (int i = WG_TID; i < m; i += WG_NT) {
+            double ax = 0.0;
+            for (int k = P.rowptr[i]; k < P.rowptr[i + 1]; ++k) ax += L.a[k] * L.xp[P.colidx[k]];
+            L.t[i] = ax;
+            const double dr = P.dr[i];
+            const double bl = P.bl.at(i, s), bu = P.bu.at(i, s);
+            if (ax < bl && (bl - ax) / dr > ptol * (1.0 + fabs(bl / dr))) bad = true;
+            if (ax > bu && (ax - bu) / dr > ptol * (1.0 + fabs(bu / dr))) bad = true;
+            if (L.rc[i] && !(bl == bu)) {
+                const double y = -L.z[i] * dr;
+                if (L.rc[i] == 1 && y < -dtol) bad = true;
+                if (L.rc[i] == 2 && y > dtol) bad = true;
+            }
+        }
+        if (bad) L.flag[0] = 1;
+        WG_SYNC();
+        if (L.flag[0] == 0) return true;
+        if (round + 1 == rounds) break;
+        // ---- primal-dual active-set update: wrong-signed multipliers leave,
+        //      violated bounds and rows enter ----
+        for (int j = WG_TID; j < n; j += WG_NT) {
+            const double l = P.lb.at(j, s), u = P.ub.at(j, s);
+            if (l == u) continue;
+            const double x = L.xp[j], lam = L.r1[j], dc = P.dc[j];
+            const int8_t c = L.cc[j];
+            if (c == 1 && lam < -dtol) L.cc[j] = 0;
+            else if (c == 2 && lam > dtol) L.cc[j] = 0;
+            else if (c == 0 && x < l && (l - x) * dc > ptol * (1.0 + fabs(l * dc))) { L.cc[j] = 1; L.xp[j] = l; }
+            else if (c == 0 && x > u && (x - u) * dc > ptol * (1.0 + fabs(u * dc))) { L.cc[j] = 2; L.xp[j] = u; }
+        }
+        for (int i = WG_TID; i < m; i += WG_NT) {
+            const double bl = P.bl.at(i, s), bu = P.bu.at(i, s);
+            if (bl == bu) continue;
+            const double ax = L.t[i], dr = P.dr[i];
+            const double y = -L.z[i] * dr;
+            const int8_t r = L.rc[i];
+            if (r == 1 && y < -dtol) { L.rc[i] = 0; L.z[i] = 0.0; }
+            else if (r == 2 && y > dtol) { L.rc[i] = 0; L.z[i] = 0.0; }
+            else if (r == 0 && ax < bl && (bl - ax) / dr > ptol * (1.0 + fabs(bl / dr))) L.rc[i] = 1;
+            else if (r == 0 && ax > bu && (ax - bu) / dr > ptol * (1.0 + fabs(bu / dr))) L.rc[i] = 2;
+        }
+        WG_SYNC();
+    }
+    return false;
+}
+
+// A certified lane: its point becomes the solution and the next warm start
+// (adopt_polished's effect).
+PHX_HD void wg_adopt(const Prob& P, const State& St, const WgLds& L, int s) {
+    const int S = P.S;
+    for (int j = WG_TID; j < P.n; j += WG_NT) {
+        const int64_t o = ix(j, s, S);
+        const double v = L.xp[j];
+        St.xT[o] = v; St.x[o] = v; St.x0[o] = v;
+    }
+    for (int i = WG_TID; i < P.m; i += WG_NT) {
+        const int64_t o = ix(i, s, S);
+        const double v = -L.z[i];
+        St.yT[o] = v; St.y[o] = v; St.y0[o] = v;
+    }
+}
+
+}  // namespace phx

@@ -13,7 +13,7 @@ passes solver options (``iter0_solver_options`` / ``iterk_solver_options``,
 phbase.py:273-275): keys ``pdhg_max_iters``, ``pdhg_check_every``,
 ``pdhg_restart_max``, ``polish``, ``polish_refine``, ``polish_below``,
 ``kkt_tol``, ``opt_tol``, ``polish_reg``, ``warm_start``, ``ipm_after``,
-``ipm_max_it``, ``ipm_tol``, ``lane_solver``, ``as_rounds``, ``warm_passes``.
+``ipm_max_it``, ``ipm_tol``, ``lane_solver``, ``as_rounds``, ``warm_passes``, ``wg_warm``.
 """
 import ctypes
 import inspect
@@ -43,6 +43,7 @@ SOLVER_DEFAULTS = {
     "lane_solver": 1,
     "as_rounds": 4,
     "warm_passes": 1,
+    "wg_warm": 16,
 }
 
 OPTIMAL, ITER_LIMIT, NUMERIC_FAIL = 1, 2, 3
@@ -107,6 +108,7 @@ class SPOpt(SPBase):
         so.lane_solver = int(o["lane_solver"])
         so.as_rounds = int(o["as_rounds"])
         so.warm_passes = int(o["warm_passes"])
+        so.wg_warm = int(o["wg_warm"])
         return so
 
     def _set_ph_terms(self):
@@ -181,6 +183,7 @@ class SPOpt(SPBase):
                     "lane_warm_list_ms": stt.lane_warm_list_ms, "lane_certified": stt.lane_certified,
                     "lane_warm_certified": stt.lane_warm_certified,
                     "lane_first_certified": stt.lane_first_certified, "stragglers": stragglers,
+                    "wg_certified": stt.wg_certified, "wg_ms": stt.wg_ms,
                     "wall_s": time.perf_counter() - t0, "not_optimal": n_bad})
         if n_bad and gripe:
             stc = self._status.cpu().numpy()

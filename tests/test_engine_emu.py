@@ -215,3 +215,43 @@ def check_native_vs_host(lib, device, case, S=30, solver=None, fused=0):
         assert np.array_equal(a.xbar_by_node()[k][0], v[0])
     assert ca == cb and Ea == Eb and ta == tb_
     return a, b
+
+
+def test_farmer_cm10_workgroup_warm_pass(emu):
+    """farmer crops_multiplier=10 (n=120, above the lane limits: generic path).
+    The workgroup warm active-set pass (phx_wg.h) must certify the later PH
+    iterations without PDHG and give the same PH trajectory as the PDHG + polish
+    path and the oracle (ph loop pinned by test_oracle_golden.py)."""
+    S, it = 6, 4
+    kw = {"num_scens": S, "crops_multiplier": 10}
+    res = {}
+    for wg in (1, 0):
+        so = {"wg_warm": 16 * wg}
+        res[wg] = run_engine(farmer.scenario_creator, farmer.scenario_names_creator(S), kw, it, lib=emu,
+                             device="cpu", options={"iter0_solver_options": so, "iterk_solver_options": so})
+    ph1, ph0 = res[1][0], res[0][0]
+    wgc = [r["wg_certified"] for r in ph1.solve_stats]
+    assert wgc[0] == 0 and wgc[-1] == S and wgc[-2] == S, wgc
+    assert all(r["pdhg_iters"] == 0 for r in ph1.solve_stats[-2:])
+    assert all(r["wg_certified"] == 0 for r in ph0.solve_stats)
+    assert all(r["not_optimal"] == 0 for r in ph1.solve_stats)
+    assert rel(ph1.xbar_by_node()["ROOT"][0], ph0.xbar_by_node()["ROOT"][0]) < 1e-9
+    assert rel(ph1.W_array(), ph0.W_array()) < 1e-8
+    # Iter0 LPs are degenerate at crops_multiplier=10 (equal optimum, different
+    # vertices), so check as test_sslp does: trivial bound, then the last
+    # iteration's subproblems re-solved by the oracle from the engine's own W /
+    # x-bar (unique nonant optimum under the prox term)
+    o = oph.OraclePH([om.farmer("scen%d" % i, crops_multiplier=10, num_scens=S) for i in range(S)], rho=1.0)
+    assert rel(res[1][3], o.iter0()) < 1e-9
+    o.W = ph1.W_array().copy()
+    o.xbar = np.tile(ph1.xbar_by_node()["ROOT"][0], (S, 1))
+    o.W_on, o.prox_on = 1, 1
+    o.solve_loop()
+    # the optimum VALUE is the bar here: with rho = 1 against costs ~1e6 the
+    # prox curvature is tiny relative to the objective, and the oracle's HiGHS
+    # QP point (when its KKT polish does not certify) sits up to ~1e-4 away in
+    # x while its objective is WORSE than the engine's certified point
+    eo = ph1._host("obj")
+    assert rel(eo, o.obj) < 1e-8
+    assert np.all(eo <= o.obj + 1e-9 * np.abs(o.obj))
+    assert rel(ph1.nonant_values(), o.xn()) < 1e-3

@@ -231,3 +231,36 @@ def test_aircond_bf10x10x10_gpu(gpu_lib):
     assert rel(Eobj, oE) < 1e-8
     assert rel(ph.W_array(), o.W) < 1e-6
     assert len(ph.xbar_by_node()) == 111
+
+
+def test_farmer_cm10_1000_workgroup_gpu(gpu_lib):
+    """BASELINE configs[1] (farmer crops_multiplier=10, 1,000 scenarios, n=120:
+    generic path).  The workgroup warm active-set pass (k_wg_warm, phx_wg.h)
+    certifies the later PH iterations without PDHG; its trajectory equals the
+    PDHG + polish path's, and a sample re-solved by the oracle from the engine's
+    own W / x-bar agrees in optimum value to 1e-8 (the oracle's point is never
+    better; see test_engine_emu.test_farmer_cm10_workgroup_warm_pass)."""
+    S, it = 1000, 5
+    kw = {"num_scens": S, "crops_multiplier": 10}
+    res = {}
+    for wg in (1, 0):
+        so = {"wg_warm": 16 * wg}
+        res[wg] = run_engine(farmer.scenario_creator, farmer.scenario_names_creator(S), kw, it, lib=gpu_lib,
+                             options={"iter0_solver_options": so, "iterk_solver_options": so})
+    ph1, ph0 = res[1][0], res[0][0]
+    assert all(r["not_optimal"] == 0 for r in ph1.solve_stats + ph0.solve_stats)
+    wgc = [r["wg_certified"] for r in ph1.solve_stats]
+    assert wgc[0] == 0 and wgc[-1] == S, wgc
+    assert rel(ph1.xbar_by_node()["ROOT"][0], ph0.xbar_by_node()["ROOT"][0]) < 1e-8
+    assert rel(ph1.W_array(), ph0.W_array()) < 1e-6
+    assert rel(res[1][2], res[0][2]) < 1e-9
+    W, xb, xn, obj = ph1.W_array(), ph1.xbar_by_node()["ROOT"][0], ph1.nonant_values(), ph1._host("obj")
+    sample = [0, 1, 2, 3, 500, 998, 999]
+    o = oph.OraclePH([om.farmer("scen%d" % k, crops_multiplier=10, num_scens=S) for k in sample], rho=1.0)
+    o.W_on = o.prox_on = 1
+    o.W[:] = W[sample]
+    o.xbar[:] = xb[None, :]
+    o.solve_loop()
+    assert rel(o.obj, obj[sample]) < 1e-8
+    assert np.all(obj[sample] <= o.obj + 1e-9 * np.abs(o.obj))
+    assert rel(o.xn(), xn[sample]) < 1e-3
