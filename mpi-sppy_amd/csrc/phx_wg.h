@@ -51,12 +51,15 @@ struct WgPairs {
 // Carve of the dynamic LDS of one scenario.
 struct WgLds {
     double *Sm, *dg, *a, *xp, *r1, *qq, *pp, *z, *t, *u;
+    int32_t *cp, *ri, *c2, *rp, *ci;   // pattern: CSC colptr/rowidx/csc2csr, CSR rowptr/colidx
+    int32_t *ar, *pos;                 // active rows (compact order) and each row's position (-1: inactive)
     int32_t* flag;
     int8_t *cc, *rc;   // column code 0 free / 1 at l / 2 at u; row code 0 inactive / 1 at bl / 2 at bu
 };
 
 PHX_HD size_t wg_lds_bytes(int n, int m, int nnz) {
-    size_t b = 8 * ((size_t)m * m + 4 * (size_t)m + (size_t)nnz + 4 * (size_t)n) + 16 + (size_t)n + (size_t)m;
+    size_t b = 8 * ((size_t)m * m + 4 * (size_t)m + (size_t)nnz + 4 * (size_t)n) +
+               4 * ((size_t)n + 1 + 3 * (size_t)nnz + (size_t)m + 1 + 2 * (size_t)m) + 16 + (size_t)n + (size_t)m;
     return (b + 15) & ~(size_t)15;
 }
 
@@ -73,7 +76,15 @@ PHX_HD WgLds wg_carve(void* base, int n, int m, int nnz) {
     L.r1 = d; d += n;
     L.qq = d; d += n;
     L.pp = d; d += n;
-    L.flag = (int32_t*)d;
+    int32_t* w = (int32_t*)d;
+    L.cp = w; w += n + 1;
+    L.ri = w; w += nnz;
+    L.c2 = w; w += nnz;
+    L.rp = w; w += m + 1;
+    L.ci = w; w += nnz;
+    L.ar = w; w += m;
+    L.pos = w; w += m;
+    L.flag = w;
     int8_t* c = (int8_t*)(L.flag + 4);
     L.cc = c; c += n;
     L.rc = c;
@@ -88,14 +99,70 @@ PHX_HD double wg_max(double v) {
     return v;
 }
 
-// Returns true (uniformly) iff the point in L.xp / L.z passes the KKT
-// certificate; rounds > 1 allow primal-dual active-set updates in between.
-PHX_HD bool wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts& O, int s, const WgLds& L,
-                    int rounds, double tol0) {
+// Optional phase timing (PHX_WG_PROF=1 on the host side): per phase, the
+// shader-clock cycles summed over the lanes' wavefronts (thread 0 of each).
+#if defined(__HIP_DEVICE_COMPILE__)
+#define WG_T0() long long _wg_t = prof ? clock64() : 0
+#define WG_TP(ph)                                                             \
+    do {                                                                      \
+        if (prof && threadIdx.x == 0) {                                       \
+            const long long _n = clock64();                                   \
+            atomicAdd(prof + (ph), (unsigned long long)(_n - _wg_t));         \
+            _wg_t = _n;                                                       \
+        }                                                                     \
+    } while (0)
+#define WG_CNT(ph) do { if (prof && threadIdx.x == 0) atomicAdd(prof + (ph), 1ull); } while (0)
+#else
+#define WG_T0() (void)prof
+#define WG_TP(ph) ((void)0)
+#define WG_CNT(ph) ((void)0)
+#endif
+
+// Order-preserving list of the active rows (ar) and each row's position in it
+// (pos, -1 when inactive); returns their count, the same on every thread.
+PHX_HD int wg_compact(const WgLds& L, int m) {
+    int cnt = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+    const int lane = (int)threadIdx.x;
+    for (int base = 0; base < m; base += 64) {
+        const int i = base + lane;
+        const bool act = i < m && L.rc[i] != 0;
+        const unsigned long long b = __ballot(act);
+        if (act) {
+            const int p = cnt + __popcll(b & ((1ull << lane) - 1ull));
+            L.ar[p] = i;
+            L.pos[i] = p;
+        } else if (i < m) {
+            L.pos[i] = -1;
+        }
+        cnt += __popcll(b);
+    }
+#else
+    for (int i = 0; i < m; ++i) {
+        if (L.rc[i]) { L.ar[cnt] = i; L.pos[i] = cnt++; }
+        else L.pos[i] = -1;
+    }
+#endif
+    return cnt;
+}
+
+// Returns (uniformly) the number of rounds the lane used when the point in
+// L.xp / L.z passes the KKT certificate, else 0; rounds > 1 allow primal-dual
+// active-set updates in between.
+PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts& O, int s, const WgLds& L,
+                   int rounds, double tol0, unsigned long long* prof = nullptr) {
+    WG_T0();
     const int S = P.S, n = P.n, m = P.m;
     const double reg = O.reg;
-    // ---- scenario data into LDS ----
-    for (int k = WG_TID; k < P.nnz; k += WG_NT) L.a[k] = aval(P, k, s);
+    // ---- scenario data and the pattern into LDS ----
+    for (int k = WG_TID; k < P.nnz; k += WG_NT) {
+        L.a[k] = aval(P, k, s);
+        L.ri[k] = P.rowidx[k];
+        L.c2[k] = P.csc2csr[k];
+        L.ci[k] = P.colidx[k];
+    }
+    for (int j = WG_TID; j <= n; j += WG_NT) L.cp[j] = P.colptr[j];
+    for (int i = WG_TID; i <= m; i += WG_NT) L.rp[i] = P.rowptr[i];
     double qm = 0.0;
     for (int j = WG_TID; j < n; j += WG_NT) {
         double q, p;
@@ -107,14 +174,14 @@ PHX_HD bool wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts
     const double dtol = O.kkt_tol * (1.0 + wg_max(qm));
     const double ptol = O.kkt_tol;
     WG_SYNC();
+    const int32_t *cp = L.cp, *ri = L.ri, *c2 = L.c2, *rp = L.rp, *ci = L.ci;
     // ---- round 0: classify the previous solution (polish_lane's rule) ----
     for (int j = WG_TID; j < n; j += WG_NT) {
         const int64_t o = ix(j, s, S);
         const double x = St.xT[o];
         const double l = P.lb.at(j, s), u = P.ub.at(j, s);
         double aty = 0.0;
-        for (int k = P.colptr[j]; k < P.colptr[j + 1]; ++k)
-            aty += L.a[P.csc2csr[k]] * St.yT[ix(P.rowidx[k], s, S)];
+        for (int k = cp[j]; k < cp[j + 1]; ++k) aty += L.a[c2[k]] * St.yT[ix(ri[k], s, S)];
         const double lam = L.qq[j] + L.pp[j] * x - aty;
         int8_t c = 0;
         if (isfinite(l) && (x - l <= tol0 * (1.0 + fabs(l)) || x - l < lam)) c = 1;
@@ -124,7 +191,7 @@ PHX_HD bool wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts
     }
     for (int i = WG_TID; i < m; i += WG_NT) {
         double ax = 0.0;
-        for (int k = P.rowptr[i]; k < P.rowptr[i + 1]; ++k) ax += L.a[k] * St.xT[ix(P.colidx[k], s, S)];
+        for (int k = rp[i]; k < rp[i + 1]; ++k) ax += L.a[k] * St.xT[ix(ci[k], s, S)];
         const double bl = P.bl.at(i, s), bu = P.bu.at(i, s);
         const double yv = St.yT[ix(i, s, S)];
         int8_t r = 0;
@@ -134,110 +201,137 @@ PHX_HD bool wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts
         L.z[i] = r ? -yv : 0.0;
     }
     WG_SYNC();
+    WG_TP(0);
     for (int round = 0; round < rounds; ++round) {
-        if (WG_TID == 0) L.flag[0] = 0;
-        // ---- Schur complement (lower part) ----
-        for (int e = WG_TID; e < m * m; e += WG_NT) {
-            const int i = e / m, k = e - i * m;
-            L.Sm[e] = (i == k) ? (L.rc[i] ? reg : 1.0) : 0.0;
+        // active rows in compact order: the Schur complement is ma x ma
+        const int ma = wg_compact(L, m);
+        if (WG_TID == 0) { L.flag[0] = 0; L.flag[1] = 0; L.flag[2] = 0; }
+        WG_SYNC();
+        // ---- Schur complement A_RF (P_FF+reg)^-1 A_RF' + reg I (lower part) ----
+        for (int e = WG_TID; e < ma * ma; e += WG_NT) {
+            const int i = e / ma, k = e - i * ma;
+            L.Sm[e] = (i == k) ? reg : 0.0;
         }
         WG_SYNC();
         for (int p = WG_TID; p < G.npair; p += WG_NT) {
-            const int ia = G.ia[p], ib = G.ib[p];
-            if (!L.rc[ia] || !L.rc[ib]) continue;
+            const int pa = L.pos[G.ia[p]], pb = L.pos[G.ib[p]];
+            if (pa < 0 || pb < 0) continue;
             double v = 0.0;
             for (int t = G.ptr[p]; t < G.ptr[p + 1]; ++t) {
-                const int ka = G.ka[t], j = P.colidx[ka];
+                const int ka = G.ka[t], j = ci[ka];
                 if (L.cc[j] == 0) v += L.a[ka] * L.a[G.kb[t]] / (L.pp[j] + reg);
             }
-            L.Sm[ia * m + ib] += v;
+            L.Sm[pa * ma + pb] += v;
         }
         WG_SYNC();
+        WG_TP(1);
         // ---- Cholesky: trailing update on the lower part, L[i][k] (i > k)
-        //      stored transposed at Sm[k*m+i], 1/diagonal in dg ----
+        //      stored transposed at Sm[k*ma+i], 1/diagonal in dg ----
         bool spd = true;
-        for (int jj = 0; jj < m; ++jj) {
-            const double d = L.Sm[jj * m + jj];
+        for (int jj = 0; jj < ma; ++jj) {
+            const double d = L.Sm[jj * ma + jj];
             if (!(d > 0.0)) { spd = false; break; }
             const double sd = sqrt(d), id = 1.0 / d;
-            for (int i = jj + 1 + WG_TID; i < m; i += WG_NT) {
-                double* row = L.Sm + (size_t)i * m;
+            for (int i = jj + 1 + WG_TID; i < ma; i += WG_NT) {
+                double* row = L.Sm + (size_t)i * ma;
                 const double lij = row[jj];
-                L.Sm[jj * m + i] = lij / sd;
+                L.Sm[jj * ma + i] = lij / sd;
                 const double f = lij * id;
                 int k = jj + 1;
                 // batches of 4: all loads issued before the stores (LDS
                 // pointers may alias as far as the compiler knows)
                 for (; k + 3 <= i; k += 4) {
-                    const double c0 = L.Sm[k * m + jj], c1 = L.Sm[(k + 1) * m + jj];
-                    const double c2 = L.Sm[(k + 2) * m + jj], c3 = L.Sm[(k + 3) * m + jj];
+                    const double g0 = L.Sm[k * ma + jj], g1 = L.Sm[(k + 1) * ma + jj];
+                    const double g2 = L.Sm[(k + 2) * ma + jj], g3 = L.Sm[(k + 3) * ma + jj];
                     const double r0 = row[k], r1 = row[k + 1], r2 = row[k + 2], r3 = row[k + 3];
-                    row[k] = r0 - f * c0; row[k + 1] = r1 - f * c1;
-                    row[k + 2] = r2 - f * c2; row[k + 3] = r3 - f * c3;
+                    row[k] = r0 - f * g0; row[k + 1] = r1 - f * g1;
+                    row[k + 2] = r2 - f * g2; row[k + 3] = r3 - f * g3;
                 }
-                for (; k <= i; ++k) row[k] -= f * L.Sm[k * m + jj];
+                for (; k <= i; ++k) row[k] -= f * L.Sm[k * ma + jj];
             }
             if (WG_TID == 0) L.dg[jj] = 1.0 / sd;
             WG_SYNC();
         }
-        if (!spd) return false;
+        if (!spd) return 0;
+        WG_TP(2);
         // ---- explicit inverse of L into the lower part (diagonal included):
         //      one column per thread, no cross-thread dependence ----
-        for (int c = WG_TID; c < m; c += WG_NT) {
-            L.Sm[c * m + c] = L.dg[c];
-            for (int i = c + 1; i < m; ++i) {
+        for (int c = WG_TID; c < ma; c += WG_NT) {
+            L.Sm[c * ma + c] = L.dg[c];
+            for (int i = c + 1; i < ma; ++i) {
                 double v = 0.0;
-                for (int k = c; k < i; ++k) v += L.Sm[k * m + i] * L.Sm[k * m + c];
-                L.Sm[i * m + c] = -v * L.dg[i];
+                for (int k = c; k < i; ++k) v += L.Sm[k * ma + i] * L.Sm[k * ma + c];
+                L.Sm[i * ma + c] = -v * L.dg[i];
             }
         }
         WG_SYNC();
-        // ---- iterative refinement on the unregularised KKT ----
+        WG_TP(3);
+        // ---- iterative refinement on the unregularised KKT (a proximal-point
+        //      iteration); stops once a step moves nothing beyond 1e-14 ----
         for (int it = 0; it < O.refine_steps; ++it) {
+            int32_t* moved = L.flag + 1 + (it & 1);
             for (int j = WG_TID; j < n; j += WG_NT) {
                 if (L.cc[j]) { L.r1[j] = 0.0; continue; }
                 double atz = 0.0;
-                for (int k = P.colptr[j]; k < P.colptr[j + 1]; ++k) atz += L.a[P.csc2csr[k]] * L.z[P.rowidx[k]];
+                for (int k = cp[j]; k < cp[j + 1]; ++k) atz += L.a[c2[k]] * L.z[ri[k]];
                 L.r1[j] = -L.qq[j] - L.pp[j] * L.xp[j] - atz;
             }
             WG_SYNC();
-            for (int i = WG_TID; i < m; i += WG_NT) {
-                if (!L.rc[i]) { L.t[i] = 0.0; continue; }
+            // the other parity's flag was last read before the barrier above
+            if (WG_TID == 0) L.flag[1 + ((it + 1) & 1)] = 0;
+            for (int q = WG_TID; q < ma; q += WG_NT) {
+                const int i = L.ar[q];
                 double adr = 0.0, ax = 0.0;
-                for (int k = P.rowptr[i]; k < P.rowptr[i + 1]; ++k) {
-                    const int j = P.colidx[k];
+                for (int k = rp[i]; k < rp[i + 1]; ++k) {
+                    const int j = ci[k];
                     ax += L.a[k] * L.xp[j];
                     if (!L.cc[j]) adr += L.a[k] * L.r1[j] / (L.pp[j] + reg);
                 }
                 const double b = L.rc[i] == 1 ? P.bl.at(i, s) : P.bu.at(i, s);
-                L.t[i] = adr - (b - ax);
+                L.t[q] = adr - (b - ax);
             }
             WG_SYNC();
-            // u = L^-1 t ; then t = L^-T u (dz)
-            for (int i = WG_TID; i < m; i += WG_NT) {
+            // u = L^-1 t ; then t = L^-T u (dz, compact order)
+            for (int i = WG_TID; i < ma; i += WG_NT) {
                 double v = 0.0;
-                for (int k = 0; k <= i; ++k) v += L.Sm[i * m + k] * L.t[k];
+                for (int k = 0; k <= i; ++k) v += L.Sm[i * ma + k] * L.t[k];
                 L.u[i] = v;
             }
             WG_SYNC();
-            for (int k = WG_TID; k < m; k += WG_NT) {
+            for (int k = WG_TID; k < ma; k += WG_NT) {
                 double v = 0.0;
-                for (int i = k; i < m; ++i) v += L.Sm[i * m + k] * L.u[i];
+                for (int i = k; i < ma; ++i) v += L.Sm[i * ma + k] * L.u[i];
                 L.t[k] = v;
             }
             WG_SYNC();
+            bool mv = false;
             for (int j = WG_TID; j < n; j += WG_NT) {
                 if (L.cc[j]) continue;
                 double atz = 0.0;
-                for (int k = P.colptr[j]; k < P.colptr[j + 1]; ++k) atz += L.a[P.csc2csr[k]] * L.t[P.rowidx[k]];
-                L.xp[j] += (L.r1[j] - atz) / (L.pp[j] + reg);
+                for (int k = cp[j]; k < cp[j + 1]; ++k) {
+                    const int q = L.pos[ri[k]];
+                    if (q >= 0) atz += L.a[c2[k]] * L.t[q];
+                }
+                const double dx = (L.r1[j] - atz) / (L.pp[j] + reg);
+                const double x = L.xp[j] + dx;
+                L.xp[j] = x;
+                if (fabs(dx) > 1e-14 * (1.0 + fabs(x))) mv = true;
             }
-            for (int i = WG_TID; i < m; i += WG_NT)
-                if (L.rc[i]) L.z[i] += L.t[i];
+            for (int q = WG_TID; q < ma; q += WG_NT) {
+                const int i = L.ar[q];
+                const double zn = L.z[i] + L.t[q];
+                if (fabs(L.t[q]) > 1e-14 * (1.0 + fabs(zn))) mv = true;
+                L.z[i] = zn;
+            }
+            if (mv) *moved = 1;
             WG_SYNC();
+            WG_CNT(8);
+            if (*moved == 0) break;
         }
+        WG_TP(4);
+        WG_CNT(9);
         // ---- certificate (polish_lane's, unscaled quantities); keeps the
-        //      multipliers (r1) and row activities (t) for the update ----
+        //      multipliers (r1) and row activities (u) for the update ----
         bool bad = false;
         for (int j = WG_TID; j < n; j += WG_NT) {
             const double x = L.xp[j];
@@ -246,7 +340,7 @@ PHX_HD bool wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts
             if (x < l && (l - x) * dc > ptol * (1.0 + fabs(l * dc))) bad = true;
             if (x > u && (x - u) * dc > ptol * (1.0 + fabs(u * dc))) bad = true;
             double atz = 0.0;
-            for (int k = P.colptr[j]; k < P.colptr[j + 1]; ++k) atz += L.a[P.csc2csr[k]] * L.z[P.rowidx[k]];
+            for (int k = cp[j]; k < cp[j + 1]; ++k) atz += L.a[c2[k]] * L.z[ri[k]];
             const double lam = (L.qq[j] + L.pp[j] * x + atz) / dc;
             L.r1[j] = lam;
             const int8_t c = L.cc[j];
@@ -259,8 +353,8 @@ PHX_HD bool wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts
         }
         for (int i = WG_TID; i < m; i += WG_NT) {
             double ax = 0.0;
-            for (int k = P.rowptr[i]; k < P.rowptr[i + 1]; ++k) ax += L.a[k] * L.xp[P.colidx[k]];
-            L.t[i] = ax;
+            for (int k = rp[i]; k < rp[i + 1]; ++k) ax += L.a[k] * L.xp[ci[k]];
+            L.u[i] = ax;
             const double dr = P.dr[i];
             const double bl = P.bl.at(i, s), bu = P.bu.at(i, s);
             if (ax < bl && (bl - ax) / dr > ptol * (1.0 + fabs(bl / dr))) bad = true;
@@ -273,7 +367,8 @@ PHX_HD bool wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts
         }
         if (bad) L.flag[0] = 1;
         WG_SYNC();
-        if (L.flag[0] == 0) return true;
+        WG_TP(5);
+        if (L.flag[0] == 0) return round + 1;
         if (round + 1 == rounds) break;
         // ---- primal-dual active-set update: wrong-signed multipliers leave,
         //      violated bounds and rows enter ----
@@ -290,7 +385,7 @@ PHX_HD bool wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts
         for (int i = WG_TID; i < m; i += WG_NT) {
             const double bl = P.bl.at(i, s), bu = P.bu.at(i, s);
             if (bl == bu) continue;
-            const double ax = L.t[i], dr = P.dr[i];
+            const double ax = L.u[i], dr = P.dr[i];
             const double y = -L.z[i] * dr;
             const int8_t r = L.rc[i];
             if (r == 1 && y < -dtol) { L.rc[i] = 0; L.z[i] = 0.0; }
@@ -299,8 +394,9 @@ PHX_HD bool wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts
             else if (r == 0 && ax > bu && (ax - bu) / dr > ptol * (1.0 + fabs(bu / dr))) L.rc[i] = 2;
         }
         WG_SYNC();
+        WG_TP(6);
     }
-    return false;
+    return 0;
 }
 
 // A certified lane: its point becomes the solution and the next warm start

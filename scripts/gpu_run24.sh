@@ -1,0 +1,8 @@
+#!/bin/bash
+# k_wg_warm phase timing (PHX_WG_PROF=1) on farmer cm=10 x1000
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+PHX_WG_PROF=1 timeout -k 10 300 python bench.py --no-cpu-baseline --cm 10 --scens 1000 --steps 5 --warmup 3 > gpurun_out/bench24_prof.log 2>&1 || { echo "BENCH FAILED"; tail -30 gpurun_out/bench24_prof.log; exit 1; }
+grep "wg prof" gpurun_out/bench24_prof.log | tail -6
