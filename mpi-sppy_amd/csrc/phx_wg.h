@@ -51,15 +51,18 @@ struct WgPairs {
 // Carve of the dynamic LDS of one scenario.
 struct WgLds {
     double *Sm, *dg, *a, *xp, *r1, *qq, *pp, *z, *t, *u;
-    int32_t *cp, *ri, *c2, *rp, *ci;   // pattern: CSC colptr/rowidx/csc2csr, CSR rowptr/colidx
-    int32_t *ar, *pos;                 // active rows (compact order) and each row's position (-1: inactive)
+    // 16-bit indices (wg_lds_bytes: nnz, n, m < 32768) keep farmer cm=10's
+    // carve under 40 KiB, i.e. four scenarios per CU
+    int16_t *cp, *ri, *c2, *rp, *ci;   // pattern: CSC colptr/rowidx/csc2csr, CSR rowptr/colidx
+    int16_t *ar, *pos;                 // active rows (compact order) and each row's position (-1: inactive)
     int32_t* flag;
     int8_t *cc, *rc;   // column code 0 free / 1 at l / 2 at u; row code 0 inactive / 1 at bl / 2 at bu
 };
 
 PHX_HD size_t wg_lds_bytes(int n, int m, int nnz) {
-    size_t b = 8 * ((size_t)m * m + 4 * (size_t)m + (size_t)nnz + 4 * (size_t)n) +
-               4 * ((size_t)n + 1 + 3 * (size_t)nnz + (size_t)m + 1 + 2 * (size_t)m) + 16 + (size_t)n + (size_t)m;
+    if (n >= 32767 || m >= 32767 || nnz >= 32767) return ~(size_t)0;   // 16-bit indices
+    size_t b = 8 * ((size_t)m * m + 4 * (size_t)m + (size_t)nnz + 4 * (size_t)n) + 16 +
+               2 * ((size_t)n + 1 + 3 * (size_t)nnz + (size_t)m + 1 + 2 * (size_t)m) + (size_t)n + (size_t)m;
     return (b + 15) & ~(size_t)15;
 }
 
@@ -76,7 +79,8 @@ PHX_HD WgLds wg_carve(void* base, int n, int m, int nnz) {
     L.r1 = d; d += n;
     L.qq = d; d += n;
     L.pp = d; d += n;
-    int32_t* w = (int32_t*)d;
+    L.flag = (int32_t*)d;
+    int16_t* w = (int16_t*)(L.flag + 4);
     L.cp = w; w += n + 1;
     L.ri = w; w += nnz;
     L.c2 = w; w += nnz;
@@ -84,8 +88,7 @@ PHX_HD WgLds wg_carve(void* base, int n, int m, int nnz) {
     L.ci = w; w += nnz;
     L.ar = w; w += m;
     L.pos = w; w += m;
-    L.flag = w;
-    int8_t* c = (int8_t*)(L.flag + 4);
+    int8_t* c = (int8_t*)w;
     L.cc = c; c += n;
     L.rc = c;
     return L;
@@ -130,8 +133,8 @@ PHX_HD int wg_compact(const WgLds& L, int m) {
         const unsigned long long b = __ballot(act);
         if (act) {
             const int p = cnt + __popcll(b & ((1ull << lane) - 1ull));
-            L.ar[p] = i;
-            L.pos[i] = p;
+            L.ar[p] = (int16_t)i;
+            L.pos[i] = (int16_t)p;
         } else if (i < m) {
             L.pos[i] = -1;
         }
@@ -139,7 +142,7 @@ PHX_HD int wg_compact(const WgLds& L, int m) {
     }
 #else
     for (int i = 0; i < m; ++i) {
-        if (L.rc[i]) { L.ar[cnt] = i; L.pos[i] = cnt++; }
+        if (L.rc[i]) { L.ar[cnt] = (int16_t)i; L.pos[i] = (int16_t)cnt++; }
         else L.pos[i] = -1;
     }
 #endif
@@ -157,12 +160,12 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
     // ---- scenario data and the pattern into LDS ----
     for (int k = WG_TID; k < P.nnz; k += WG_NT) {
         L.a[k] = aval(P, k, s);
-        L.ri[k] = P.rowidx[k];
-        L.c2[k] = P.csc2csr[k];
-        L.ci[k] = P.colidx[k];
+        L.ri[k] = (int16_t)P.rowidx[k];
+        L.c2[k] = (int16_t)P.csc2csr[k];
+        L.ci[k] = (int16_t)P.colidx[k];
     }
-    for (int j = WG_TID; j <= n; j += WG_NT) L.cp[j] = P.colptr[j];
-    for (int i = WG_TID; i <= m; i += WG_NT) L.rp[i] = P.rowptr[i];
+    for (int j = WG_TID; j <= n; j += WG_NT) L.cp[j] = (int16_t)P.colptr[j];
+    for (int i = WG_TID; i <= m; i += WG_NT) L.rp[i] = (int16_t)P.rowptr[i];
     double qm = 0.0;
     for (int j = WG_TID; j < n; j += WG_NT) {
         double q, p;
@@ -174,7 +177,7 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
     const double dtol = O.kkt_tol * (1.0 + wg_max(qm));
     const double ptol = O.kkt_tol;
     WG_SYNC();
-    const int32_t *cp = L.cp, *ri = L.ri, *c2 = L.c2, *rp = L.rp, *ci = L.ci;
+    const int16_t *cp = L.cp, *ri = L.ri, *c2 = L.c2, *rp = L.rp, *ci = L.ci;
     // ---- round 0: classify the previous solution (polish_lane's rule) ----
     for (int j = WG_TID; j < n; j += WG_NT) {
         const int64_t o = ix(j, s, S);
@@ -259,17 +262,24 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
         for (int c = WG_TID; c < ma; c += WG_NT) {
             L.Sm[c * ma + c] = L.dg[c];
             for (int i = c + 1; i < ma; ++i) {
-                double v = 0.0;
-                for (int k = c; k < i; ++k) v += L.Sm[k * ma + i] * L.Sm[k * ma + c];
-                L.Sm[i * ma + c] = -v * L.dg[i];
+                // four partial sums: four LDS load pairs in flight per step
+                double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
+                int k = c;
+                for (; k + 3 < i; k += 4) {
+                    v0 += L.Sm[k * ma + i] * L.Sm[k * ma + c];
+                    v1 += L.Sm[(k + 1) * ma + i] * L.Sm[(k + 1) * ma + c];
+                    v2 += L.Sm[(k + 2) * ma + i] * L.Sm[(k + 2) * ma + c];
+                    v3 += L.Sm[(k + 3) * ma + i] * L.Sm[(k + 3) * ma + c];
+                }
+                for (; k < i; ++k) v0 += L.Sm[k * ma + i] * L.Sm[k * ma + c];
+                L.Sm[i * ma + c] = -((v0 + v1) + (v2 + v3)) * L.dg[i];
             }
         }
         WG_SYNC();
         WG_TP(3);
         // ---- iterative refinement on the unregularised KKT (a proximal-point
-        //      iteration); stops once a step moves nothing beyond 1e-14 ----
+        //      iteration) ----
         for (int it = 0; it < O.refine_steps; ++it) {
-            int32_t* moved = L.flag + 1 + (it & 1);
             for (int j = WG_TID; j < n; j += WG_NT) {
                 if (L.cc[j]) { L.r1[j] = 0.0; continue; }
                 double atz = 0.0;
@@ -277,8 +287,6 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
                 L.r1[j] = -L.qq[j] - L.pp[j] * L.xp[j] - atz;
             }
             WG_SYNC();
-            // the other parity's flag was last read before the barrier above
-            if (WG_TID == 0) L.flag[1 + ((it + 1) & 1)] = 0;
             for (int q = WG_TID; q < ma; q += WG_NT) {
                 const int i = L.ar[q];
                 double adr = 0.0, ax = 0.0;
@@ -293,18 +301,33 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
             WG_SYNC();
             // u = L^-1 t ; then t = L^-T u (dz, compact order)
             for (int i = WG_TID; i < ma; i += WG_NT) {
-                double v = 0.0;
-                for (int k = 0; k <= i; ++k) v += L.Sm[i * ma + k] * L.t[k];
-                L.u[i] = v;
+                double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
+                const double* row = L.Sm + (size_t)i * ma;
+                int k = 0;
+                for (; k + 3 <= i; k += 4) {
+                    v0 += row[k] * L.t[k];
+                    v1 += row[k + 1] * L.t[k + 1];
+                    v2 += row[k + 2] * L.t[k + 2];
+                    v3 += row[k + 3] * L.t[k + 3];
+                }
+                for (; k <= i; ++k) v0 += row[k] * L.t[k];
+                L.u[i] = (v0 + v1) + (v2 + v3);
             }
             WG_SYNC();
             for (int k = WG_TID; k < ma; k += WG_NT) {
-                double v = 0.0;
-                for (int i = k; i < ma; ++i) v += L.Sm[i * ma + k] * L.u[i];
-                L.t[k] = v;
+                double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
+                int i = k;
+                for (; i + 3 < ma; i += 4) {
+                    v0 += L.Sm[i * ma + k] * L.u[i];
+                    v1 += L.Sm[(i + 1) * ma + k] * L.u[i + 1];
+                    v2 += L.Sm[(i + 2) * ma + k] * L.u[i + 2];
+                    v3 += L.Sm[(i + 3) * ma + k] * L.u[i + 3];
+                }
+                for (; i < ma; ++i) v0 += L.Sm[i * ma + k] * L.u[i];
+                L.t[k] = (v0 + v1) + (v2 + v3);
             }
             WG_SYNC();
-            bool mv = false;
+            double dmax = 0.0, xmax = 0.0;
             for (int j = WG_TID; j < n; j += WG_NT) {
                 if (L.cc[j]) continue;
                 double atz = 0.0;
@@ -315,18 +338,21 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
                 const double dx = (L.r1[j] - atz) / (L.pp[j] + reg);
                 const double x = L.xp[j] + dx;
                 L.xp[j] = x;
-                if (fabs(dx) > 1e-14 * (1.0 + fabs(x))) mv = true;
+                dmax = fmax(dmax, fabs(dx));
+                xmax = fmax(xmax, fabs(x));
             }
             for (int q = WG_TID; q < ma; q += WG_NT) {
                 const int i = L.ar[q];
                 const double zn = L.z[i] + L.t[q];
-                if (fabs(L.t[q]) > 1e-14 * (1.0 + fabs(zn))) mv = true;
+                dmax = fmax(dmax, fabs(L.t[q]));
+                xmax = fmax(xmax, fabs(zn));
                 L.z[i] = zn;
             }
-            if (mv) *moved = 1;
+            // stop once the correction vanishes (phx_lane.h kkt_refine's rule)
+            const bool done = wg_max(dmax) <= 1e-10 * (1.0 + wg_max(xmax));
             WG_SYNC();
             WG_CNT(8);
-            if (*moved == 0) break;
+            if (done) break;
         }
         WG_TP(4);
         WG_CNT(9);
