@@ -61,7 +61,7 @@ struct WgLds {
 
 PHX_HD size_t wg_lds_bytes(int n, int m, int nnz) {
     if (n >= 32767 || m >= 32767 || nnz >= 32767) return ~(size_t)0;   // 16-bit indices
-    size_t b = 8 * ((size_t)m * m + 4 * (size_t)m + (size_t)nnz + 4 * (size_t)n) + 16 +
+    size_t b = 8 * ((size_t)m * (m + 1) + 4 * (size_t)m + (size_t)nnz + 4 * (size_t)n) + 16 +
                2 * ((size_t)n + 1 + 3 * (size_t)nnz + (size_t)m + 1 + 2 * (size_t)m) + (size_t)n + (size_t)m;
     return (b + 15) & ~(size_t)15;
 }
@@ -69,7 +69,7 @@ PHX_HD size_t wg_lds_bytes(int n, int m, int nnz) {
 PHX_HD WgLds wg_carve(void* base, int n, int m, int nnz) {
     WgLds L;
     double* d = (double*)base;
-    L.Sm = d; d += (size_t)m * m;
+    L.Sm = d; d += (size_t)m * (m + 1);   // rows padded to an odd stride (wg_warm)
     L.dg = d; d += m;
     L.z = d; d += m;
     L.t = d; d += m;
@@ -210,9 +210,13 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
         const int ma = wg_compact(L, m);
         if (WG_TID == 0) { L.flag[0] = 0; L.flag[1] = 0; L.flag[2] = 0; }
         WG_SYNC();
-        // ---- Schur complement A_RF (P_FF+reg)^-1 A_RF' + reg I (lower part) ----
-        for (int e = WG_TID; e < ma * ma; e += WG_NT) {
-            const int i = e / ma, k = e - i * ma;
+        // ---- Schur complement A_RF (P_FF+reg)^-1 A_RF' + reg I (lower part).
+        //      Row stride ld = ma | 1 (odd): a wavefront reading one column of
+        //      64 rows hits distinct LDS banks (an even stride of 40 doubles
+        //      made that a 16-way conflict) ----
+        const int ld = ma | 1;
+        for (int e = WG_TID; e < ma * ld; e += WG_NT) {
+            const int i = e / ld, k = e - i * ld;
             L.Sm[e] = (i == k) ? reg : 0.0;
         }
         WG_SYNC();
@@ -224,33 +228,33 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
                 const int ka = G.ka[t], j = ci[ka];
                 if (L.cc[j] == 0) v += L.a[ka] * L.a[G.kb[t]] / (L.pp[j] + reg);
             }
-            L.Sm[pa * ma + pb] += v;
+            L.Sm[pa * ld + pb] += v;
         }
         WG_SYNC();
         WG_TP(1);
         // ---- Cholesky: trailing update on the lower part, L[i][k] (i > k)
-        //      stored transposed at Sm[k*ma+i], 1/diagonal in dg ----
+        //      stored transposed at Sm[k*ld+i], 1/diagonal in dg ----
         bool spd = true;
         for (int jj = 0; jj < ma; ++jj) {
-            const double d = L.Sm[jj * ma + jj];
+            const double d = L.Sm[jj * ld + jj];
             if (!(d > 0.0)) { spd = false; break; }
             const double sd = sqrt(d), id = 1.0 / d;
             for (int i = jj + 1 + WG_TID; i < ma; i += WG_NT) {
-                double* row = L.Sm + (size_t)i * ma;
+                double* row = L.Sm + (size_t)i * ld;
                 const double lij = row[jj];
-                L.Sm[jj * ma + i] = lij / sd;
+                L.Sm[jj * ld + i] = lij / sd;
                 const double f = lij * id;
                 int k = jj + 1;
                 // batches of 4: all loads issued before the stores (LDS
                 // pointers may alias as far as the compiler knows)
                 for (; k + 3 <= i; k += 4) {
-                    const double g0 = L.Sm[k * ma + jj], g1 = L.Sm[(k + 1) * ma + jj];
-                    const double g2 = L.Sm[(k + 2) * ma + jj], g3 = L.Sm[(k + 3) * ma + jj];
+                    const double g0 = L.Sm[k * ld + jj], g1 = L.Sm[(k + 1) * ld + jj];
+                    const double g2 = L.Sm[(k + 2) * ld + jj], g3 = L.Sm[(k + 3) * ld + jj];
                     const double r0 = row[k], r1 = row[k + 1], r2 = row[k + 2], r3 = row[k + 3];
                     row[k] = r0 - f * g0; row[k + 1] = r1 - f * g1;
                     row[k + 2] = r2 - f * g2; row[k + 3] = r3 - f * g3;
                 }
-                for (; k <= i; ++k) row[k] -= f * L.Sm[k * ma + jj];
+                for (; k <= i; ++k) row[k] -= f * L.Sm[k * ld + jj];
             }
             if (WG_TID == 0) L.dg[jj] = 1.0 / sd;
             WG_SYNC();
@@ -260,19 +264,19 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
         // ---- explicit inverse of L into the lower part (diagonal included):
         //      one column per thread, no cross-thread dependence ----
         for (int c = WG_TID; c < ma; c += WG_NT) {
-            L.Sm[c * ma + c] = L.dg[c];
+            L.Sm[c * ld + c] = L.dg[c];
             for (int i = c + 1; i < ma; ++i) {
                 // four partial sums: four LDS load pairs in flight per step
                 double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
                 int k = c;
                 for (; k + 3 < i; k += 4) {
-                    v0 += L.Sm[k * ma + i] * L.Sm[k * ma + c];
-                    v1 += L.Sm[(k + 1) * ma + i] * L.Sm[(k + 1) * ma + c];
-                    v2 += L.Sm[(k + 2) * ma + i] * L.Sm[(k + 2) * ma + c];
-                    v3 += L.Sm[(k + 3) * ma + i] * L.Sm[(k + 3) * ma + c];
+                    v0 += L.Sm[k * ld + i] * L.Sm[k * ld + c];
+                    v1 += L.Sm[(k + 1) * ld + i] * L.Sm[(k + 1) * ld + c];
+                    v2 += L.Sm[(k + 2) * ld + i] * L.Sm[(k + 2) * ld + c];
+                    v3 += L.Sm[(k + 3) * ld + i] * L.Sm[(k + 3) * ld + c];
                 }
-                for (; k < i; ++k) v0 += L.Sm[k * ma + i] * L.Sm[k * ma + c];
-                L.Sm[i * ma + c] = -((v0 + v1) + (v2 + v3)) * L.dg[i];
+                for (; k < i; ++k) v0 += L.Sm[k * ld + i] * L.Sm[k * ld + c];
+                L.Sm[i * ld + c] = -((v0 + v1) + (v2 + v3)) * L.dg[i];
             }
         }
         WG_SYNC();
@@ -302,7 +306,7 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
             // u = L^-1 t ; then t = L^-T u (dz, compact order)
             for (int i = WG_TID; i < ma; i += WG_NT) {
                 double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
-                const double* row = L.Sm + (size_t)i * ma;
+                const double* row = L.Sm + (size_t)i * ld;
                 int k = 0;
                 for (; k + 3 <= i; k += 4) {
                     v0 += row[k] * L.t[k];
@@ -318,12 +322,12 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
                 double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
                 int i = k;
                 for (; i + 3 < ma; i += 4) {
-                    v0 += L.Sm[i * ma + k] * L.u[i];
-                    v1 += L.Sm[(i + 1) * ma + k] * L.u[i + 1];
-                    v2 += L.Sm[(i + 2) * ma + k] * L.u[i + 2];
-                    v3 += L.Sm[(i + 3) * ma + k] * L.u[i + 3];
+                    v0 += L.Sm[i * ld + k] * L.u[i];
+                    v1 += L.Sm[(i + 1) * ld + k] * L.u[i + 1];
+                    v2 += L.Sm[(i + 2) * ld + k] * L.u[i + 2];
+                    v3 += L.Sm[(i + 3) * ld + k] * L.u[i + 3];
                 }
-                for (; i < ma; ++i) v0 += L.Sm[i * ma + k] * L.u[i];
+                for (; i < ma; ++i) v0 += L.Sm[i * ld + k] * L.u[i];
                 L.t[k] = (v0 + v1) + (v2 + v3);
             }
             WG_SYNC();
