@@ -264,3 +264,11 @@ def test_farmer_cm10_1000_workgroup_gpu(gpu_lib):
     assert rel(o.obj, obj[sample]) < 1e-8
     assert np.all(obj[sample] <= o.obj + 1e-9 * np.abs(o.obj))
     assert rel(o.xn(), xn[sample]) < 1e-3
+
+
+def test_wxbar_writer_reader_gpu(gpu_lib, tmp_path):
+    """W / x-bar CSV checkpoint I/O through the device state: the reference's
+    fixture and asserts (test_w_writer.py), see tests/test_wxbar.py."""
+    import test_wxbar as tw
+    tw.check_writer(gpu_lib, None, tmp_path)
+    tw.check_reader(gpu_lib, None)
