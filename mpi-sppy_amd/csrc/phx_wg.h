@@ -429,6 +429,50 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
     return 0;
 }
 
+// sum over the workgroup (one wavefront: butterfly), identity on the host
+PHX_HD double wg_sum(double v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+#endif
+    return v;
+}
+
+// A certified lane's outputs, as finalize_lane (phx_core.h) writes them:
+// unscaled x and row duals, objective c'x + qN'x_N + pN x_N^2 / 2 + kN.
+PHX_HD void wg_write_out(const Prob& P, const WgLds& L, const double* c_unscaled_p, int64_t c_si, int64_t c_ss,
+                         int s, double* x_out, double* y_out, double* obj_out) {
+    const int S = P.S;
+    double f = 0.0;
+    for (int j = WG_TID; j < P.n; j += WG_NT) {
+        const double x = L.xp[j] * P.dc[j];
+        x_out[ix(j, s, S)] = x;
+        f += c_unscaled_p[(int64_t)j * c_si + (int64_t)s * c_ss] * x;
+        const int sl = P.col_slot[j];
+        if (sl >= 0) f += P.qN[ix(sl, s, S)] * x + 0.5 * P.pN[ix(sl, s, S)] * x * x;
+    }
+    if (y_out)
+        for (int i = WG_TID; i < P.m; i += WG_NT) y_out[ix(i, s, S)] = -L.z[i] * P.dr[i];
+    f = wg_sum(f);
+    if (WG_TID == 0) obj_out[s] = P.kN[s] + f;
+}
+
+// A lane the pass leaves to PDHG: k_begin_solve's warm start (mode 1) for it,
+// which the pass replaces when it runs.
+PHX_HD void wg_begin_generic(const Prob& P, const State& St, int s) {
+    const int S = P.S;
+    for (int j = WG_TID; j < P.n; j += WG_NT) St.x0[ix(j, s, S)] = St.x[ix(j, s, S)];
+    for (int i = WG_TID; i < P.m; i += WG_NT) St.y0[ix(i, s, S)] = St.y[ix(i, s, S)];
+    if (WG_TID == 0) {
+        St.hk[s] = 0;
+        St.r0[s] = 1e301;
+        St.rprev[s] = 1e301;
+        St.status[s] = RUNNING;
+        St.iters[s] = 0;
+        St.err[s] = 1e300;
+        St.flags[s] = 0;
+    }
+}
+
 // A certified lane: its point becomes the solution and the next warm start
 // (adopt_polished's effect).
 PHX_HD void wg_adopt(const Prob& P, const State& St, const WgLds& L, int s) {
