@@ -291,3 +291,38 @@ def sslp(sname, instance=None, num_scens=None):
         bl[ns + i] = bu[ns + i] = present[i]
     prob = 1.0 / num_scens if num_scens is not None else None
     return Scen(sname, names, c, 0.0, A, bl, bu, lb, ub, [("ROOT", 1.0, 1, list(range(ns)))], prob)
+
+
+# ---------------------------------------------------------------- netdes
+def netdes(sname, instance="network-10-10-H-01", num_scens=None):
+    """netdes LP relaxation (``examples/netdes/netdes.py:32-71``): x[e] in [0,1] then
+    y[e] >= 0 per edge (edges = row-major nonzeros of the adjacency matrix,
+    ``parse.py:58-59``); rows vubs y_e - u_e x_e <= 0, then bals (out-flow minus in-flow
+    == b_i per node); cost c'x + d'y.  Data from the reference's .dat file (extracted to
+    netdes_<instance>.npz); scenario index = trailing digits of the name (netdes.py:79-87);
+    indices >= K take shipped scenario k mod K with d scaled by 1 + 0.2 (r - 1/2),
+    r ~ RandomState(k).rand(E) (the build's synthetic workload)."""
+    f = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "mpi-sppy_amd", "examples",
+                     "data", "netdes_%s.npz" % instance)
+    z = np.load(f)
+    k = int(re.search(r"(\d+)$", sname).group(1))
+    K = len(z["p"])
+    ed = z["edges"]
+    E, N = len(ed), int(z["N"])
+    d, u, b = z["d"][k % K], z["u"][k % K], z["b"][k % K]
+    if k >= K:
+        d = d * (1.0 + 0.2 * (np.random.RandomState(k).rand(E) - 0.5))
+    A = np.zeros((E + N, 2 * E))
+    for e in range(E):
+        A[e, e] = -u[e]
+        A[e, E + e] = 1.0
+        A[E + ed[e, 0], E + e] += 1.0
+        A[E + ed[e, 1], E + e] -= 1.0
+    bl = np.concatenate([np.full(E, -INF), b])
+    bu = np.concatenate([np.zeros(E), b])
+    names = ["x[%d,%d]" % (i, j) for i, j in ed] + ["y[%d,%d]" % (i, j) for i, j in ed]
+    lb = np.zeros(2 * E)
+    ub = np.concatenate([np.ones(E), np.full(E, INF)])
+    prob = 1.0 / num_scens if num_scens is not None else (float(z["p"][k]) if k < K else None)
+    return Scen(sname, names, np.concatenate([z["c"], d]), 0.0, A, bl, bu, lb, ub,
+                [("ROOT", 1.0, 1, list(range(E)))], prob)

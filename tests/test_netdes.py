@@ -1,0 +1,100 @@
+"""netdes LP relaxation (workload C5b): the restated scenario creator
+(batch == per-scenario models, bit-exact; == the oracle's dense restatement), and PH
+through the engine against the oracle on the shipped network-10-10-H-01 instance
+(n = 108, m = 64, 54 nonants, scenario-varying A, c and right-hand sides, shipped
+non-uniform probabilities).  The reference ships no netdes LP-relaxation golden values
+(solutions.dat holds MIP optima; asserted here only as an upper bound on the LP
+trivial bound): parity is engine vs the oracle restatement, whose PH loop is pinned by
+the farmer/aircond goldens (test_oracle_golden.py)."""
+import numpy as np
+import pytest
+
+from helpers import rel, run_engine
+from mpisppy_amd.batch import from_models
+from mpisppy_amd.examples import netdes
+from oracle import models as om, ph as oph
+
+INST = "network-10-10-H-01"
+MIP_OPT = 27523.7          # examples/netdes/solutions.dat, network-10-10-H-01 best bound
+
+
+def test_netdes_batch_equals_models():
+    names = netdes.scenario_names_creator(12)       # Scenario0..9 shipped, 10..11 synthetic
+    a = from_models(names, [netdes.scenario_creator(nm, path="data/%s.dat" % INST) for nm in names]).compress()
+    b = netdes.batch_creator(names, instance=INST).compress()
+    for k in ["rowptr", "colidx", "kvar", "Aconst", "Avar", "c", "lb", "ub", "bl", "bu"]:
+        assert np.array_equal(getattr(a, k), getattr(b, k)), k
+    assert (a.n, a.m) == (108, 64) and a.nnz == b.nnz == 2 * 54 + 2 * 54
+    assert list(a.nonant.slot_col) == list(range(54)) and a.rhs_vary and a.c_vary
+    assert a.prob == b.prob and abs(sum(a.prob[:10]) - 1.0) < 1e-12 and a.prob[10] is None
+    with pytest.raises(RuntimeError):
+        netdes.scenario_creator("Scenario0")
+    assert netdes._get_scenario_ix("Scen07") == 7
+
+
+def test_netdes_oracle_model_matches_creator():
+    for nm in ["Scenario3", "Scenario17"]:
+        sf = netdes.scenario_creator(nm, instance=INST).standard_form()
+        o = om.netdes(nm, INST)
+        A = np.zeros((len(sf["bl"]), len(sf["c"])))
+        for i in range(len(sf["bl"])):
+            for k in range(sf["rowptr"][i], sf["rowptr"][i + 1]):
+                A[i, sf["colidx"][k]] = sf["vals"][k]
+        assert np.array_equal(A, o.A) and np.array_equal(sf["c"], o.c)
+        assert np.array_equal(sf["bl"], o.bl) and np.array_equal(sf["bu"], o.bu)
+        assert np.array_equal(sf["lb"], o.lb) and np.array_equal(sf["ub"], o.ub)
+
+
+def test_netdes_oracle_trivial_bound_below_mip():
+    o = oph.OraclePH([om.netdes(nm, INST) for nm in netdes.scenario_names_creator(10)], rho=1.0)
+    tb = o.iter0()
+    assert 0.0 < tb <= MIP_OPT
+
+
+def check_netdes_ph(lib, device, iters=3):
+    """Iter0 LPs may be degenerate, so engine and oracle trajectories can differ;
+    checked: the trivial bound (unique LP optimum value) to 1e-8, and every subproblem
+    of the last iteration re-solved by the oracle from the engine's own W / x-bar: the
+    nonants to 1e-6 and the objectives to 1e-8 (north_star bar)."""
+    names = netdes.scenario_names_creator(10)
+    ph, conv, Eobj, tb = run_engine(netdes.scenario_creator, names, {"instance": INST}, iters, lib=lib,
+                                    device=device, options={"per_scenario_models": True})
+    o = oph.OraclePH([om.netdes(nm, INST) for nm in names], rho=1.0)
+    otb = o.iter0()
+    assert rel(tb, otb) < 1e-8
+    assert all(s["not_optimal"] == 0 for s in ph.solve_stats)
+    o.W = ph.W_array().copy()
+    o.xbar = np.tile(ph.xbar_by_node()["ROOT"][0], (len(names), 1))
+    o.W_on, o.prox_on = 1, 1
+    o.solve_loop()
+    assert rel(ph.nonant_values(), o.xn()) < 1e-6
+    assert rel(ph._host("obj"), o.obj) < 1e-8
+    return ph, o
+
+
+def test_netdes_ph_emu(emu):
+    check_netdes_ph(emu, "cpu", iters=2)
+
+
+@pytest.mark.gpu
+def test_netdes_ph_gpu(gpu_lib):
+    check_netdes_ph(gpu_lib, None, iters=3)
+
+
+@pytest.mark.gpu
+def test_netdes_synthetic_batch_gpu(gpu_lib):
+    """200 scenarios (10 shipped + 190 synthetic, batch creator, p = 1/200): every
+    subproblem certified; the last iteration re-solved by the oracle from the engine's
+    W / x-bar agrees to 1e-6 on a sample of scenarios."""
+    names = netdes.scenario_names_creator(200)
+    ph, conv, Eobj, tb = run_engine(netdes.scenario_creator, names, {"instance": INST, "num_scens": 200}, 3,
+                                    lib=gpu_lib)
+    assert all(s["not_optimal"] == 0 for s in ph.solve_stats)
+    pick = [0, 7, 10, 99, 199]
+    o = oph.OraclePH([om.netdes(names[k], INST, num_scens=200) for k in pick], rho=1.0)
+    o.iter0()
+    o.W = ph.W_array()[pick].copy()
+    o.xbar = np.tile(ph.xbar_by_node()["ROOT"][0], (len(pick), 1))
+    o.W_on, o.prox_on = 1, 1
+    o.solve_loop()
+    assert rel(ph.nonant_values()[pick], o.xn()) < 1e-6
