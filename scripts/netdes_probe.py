@@ -22,6 +22,8 @@ if S != 30:
 solver = {}
 if len(sys.argv) > 3:                      # pdhg_max_iters, polish
     solver = {"pdhg_max_iters": int(sys.argv[3]), "polish": int(sys.argv[4])}
+if len(sys.argv) > 5:                      # ipm_after
+    solver["ipm_after"] = int(sys.argv[5])
 t = time.time()
 
 
