@@ -100,6 +100,13 @@ typedef struct phx_solve_opts {
                                  up to k rounds from the previous solution;
                                  PDHG + polish only for the lanes it does not
                                  certify.  0: off                             */
+    int32_t sp;               /* 1: use the sparse workgroup solver (phx_sp.h:
+                                 separator Schur complement, interior point +
+                                 active-set rounds) when the context has one;
+                                 0: skip it (generic PDHG path only)          */
+    int32_t sp_rounds;        /* sparse solver: active-set rounds after its
+                                 interior point (cold) and from the previous
+                                 solution (warm)                              */
 } phx_solve_opts;
 
 /* Statistics of the most recent phx_solve (HIP events on the solve stream). */
@@ -124,6 +131,12 @@ typedef struct phx_solve_stats {
                                  affine-map pass when maps are on)            */
     int32_t wg_certified;     /* certified by the workgroup warm pass         */
     double  wg_ms;            /* workgroup warm pass kernel time              */
+    int32_t sp_certified;     /* certified by the sparse workgroup solver     */
+    int32_t sp_warm_rounds;   /* its active-set rounds from warm starts (sum) */
+    int32_t sp_ipm_its;       /* its interior-point iterations (sum)          */
+    int32_t sp_cold_rounds;   /* its active-set rounds after the IPM (sum)    */
+    int32_t sp_refine;        /* its refinement solves (sum)                  */
+    double  sp_ms;            /* sparse solver kernel time                    */
 } phx_solve_stats;
 
 /* Scenario-tree reduction layout for Compute_Xbar (phbase.py:27-107): for each

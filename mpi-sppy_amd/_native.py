@@ -40,7 +40,7 @@ class SolveOpts(ctypes.Structure):
         ("reg", c_double),
         ("ipm_after", c_int32), ("ipm_max_it", c_int32), ("ipm_tol", c_double),
         ("lane_solver", c_int32), ("as_rounds", c_int32), ("warm_passes", c_int32),
-        ("defer", c_int32), ("wg_warm", c_int32),
+        ("defer", c_int32), ("wg_warm", c_int32), ("sp", c_int32), ("sp_rounds", c_int32),
     ]
 
 
@@ -51,6 +51,8 @@ class SolveStats(ctypes.Structure):
         ("lane_iters", c_double), ("pdhg_launches", c_int32), ("total_iters", c_int32),
         ("lane_certified", c_int32), ("lane_warm_certified", c_int32), ("not_optimal", c_int32), ("stragglers", c_int32), ("jit", c_int32),
         ("lane_first_certified", c_int32), ("wg_certified", c_int32), ("wg_ms", c_double),
+        ("sp_certified", c_int32), ("sp_warm_rounds", c_int32), ("sp_ipm_its", c_int32),
+        ("sp_cold_rounds", c_int32), ("sp_refine", c_int32), ("sp_ms", c_double),
     ]
 
 

@@ -140,4 +140,104 @@ inline void build_wg_pairs(const HostSetup& hs, int n, int m, WgPairsHost& out) 
         }
 }
 
+// Symbolic structure of the sparse workgroup solver (phx_sp.h SpSym): rows
+// split into B, a maximal set of rows pairwise without a shared column (greedy,
+// fewest neighbouring rows first, then row index), and the separator C (the
+// rest, ascending row index); the B-C links with their shared columns; the
+// direct and via-B terms of every separator Schur entry.  Deterministic (all
+// lists in ascending order).  Returns false with a reason when the separator
+// exceeds max_c rows.
+struct SpSymHost {
+    int nC = 0, nlink = 0;
+    std::vector<int32_t> cpos, crow, lptr, lc, lrow, lkp, lkb, lkc, clp, cll, eap, eka, ekb, ebp, el1, el2;
+};
+
+inline bool build_sp_sym(const HostSetup& hs, int n, int m, int max_c, SpSymHost& out, std::string& why) {
+    out = SpSymHost{};
+    std::vector<std::vector<int32_t>> adj(m);
+    for (int j = 0; j < n; ++j)
+        for (int a = hs.colptr[j]; a < hs.colptr[j + 1]; ++a)
+            for (int b = hs.colptr[j]; b < hs.colptr[j + 1]; ++b)
+                if (hs.rowidx[a] != hs.rowidx[b]) adj[hs.rowidx[a]].push_back(hs.rowidx[b]);
+    for (auto& v : adj) {
+        std::sort(v.begin(), v.end());
+        v.erase(std::unique(v.begin(), v.end()), v.end());
+    }
+    std::vector<int32_t> order(m);
+    for (int i = 0; i < m; ++i) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return adj[a].size() < adj[b].size(); });
+    std::vector<char> inB(m, 0), blocked(m, 0);
+    for (int r : order) {
+        if (blocked[r]) continue;
+        inB[r] = 1;
+        for (int q : adj[r]) blocked[q] = 1;
+    }
+    out.cpos.assign(m, -1);
+    for (int i = 0; i < m; ++i)
+        if (!inB[i]) {
+            out.cpos[i] = (int32_t)out.crow.size();
+            out.crow.push_back(i);
+        }
+    out.nC = (int)out.crow.size();
+    if (out.nC > max_c) {
+        why = "separator of " + std::to_string(out.nC) + " rows > " + std::to_string(max_c);
+        return false;
+    }
+    const int nC = out.nC;
+    // links of each B row, ascending separator position; shared columns ascending
+    out.lptr.assign(1, 0);
+    out.lkp.assign(1, 0);
+    for (int b = 0; b < m; ++b) {
+        if (inB[b]) {
+            std::vector<std::vector<std::pair<int32_t, int32_t>>> lk(nC);
+            for (int kb = hs.rowptr[b]; kb < hs.rowptr[b + 1]; ++kb) {
+                const int j = hs.colidx[kb];
+                for (int q = hs.colptr[j]; q < hs.colptr[j + 1]; ++q) {
+                    const int r = hs.rowidx[q];
+                    if (r != b && out.cpos[r] >= 0) lk[out.cpos[r]].push_back({kb, hs.csc2csr[q]});
+                }
+            }
+            for (int c = 0; c < nC; ++c) {
+                if (lk[c].empty()) continue;
+                out.lc.push_back(c);
+                out.lrow.push_back(b);
+                for (const auto& pr : lk[c]) { out.lkb.push_back(pr.first); out.lkc.push_back(pr.second); }
+                out.lkp.push_back((int32_t)out.lkb.size());
+            }
+        }
+        out.lptr.push_back((int32_t)out.lc.size());
+    }
+    out.nlink = (int)out.lc.size();
+    out.clp.assign(nC + 1, 0);
+    for (int l = 0; l < out.nlink; ++l) out.clp[out.lc[l] + 1]++;
+    for (int c = 0; c < nC; ++c) out.clp[c + 1] += out.clp[c];
+    out.cll.assign(out.nlink, 0);
+    {
+        std::vector<int32_t> fill(out.clp.begin(), out.clp.end() - 1);
+        for (int l = 0; l < out.nlink; ++l) out.cll[fill[out.lc[l]]++] = l;
+    }
+    // separator Schur entries (c1 >= c2) at c1*nC + c2
+    std::vector<std::vector<std::pair<int32_t, int32_t>>> dir((size_t)nC * nC), via((size_t)nC * nC);
+    for (int j = 0; j < n; ++j)
+        for (int a = hs.colptr[j]; a < hs.colptr[j + 1]; ++a)
+            for (int b = hs.colptr[j]; b < hs.colptr[j + 1]; ++b) {
+                const int ca = out.cpos[hs.rowidx[a]], cb = out.cpos[hs.rowidx[b]];
+                if (ca < 0 || cb < 0 || ca < cb) continue;
+                dir[(size_t)ca * nC + cb].push_back({hs.csc2csr[a], hs.csc2csr[b]});
+            }
+    for (int b = 0; b < m; ++b)
+        for (int l1 = out.lptr[b]; l1 < out.lptr[b + 1]; ++l1)
+            for (int l2 = out.lptr[b]; l2 < out.lptr[b + 1]; ++l2)
+                if (out.lc[l1] >= out.lc[l2]) via[(size_t)out.lc[l1] * nC + out.lc[l2]].push_back({l1, l2});
+    out.eap.assign(1, 0);
+    out.ebp.assign(1, 0);
+    for (size_t p = 0; p < (size_t)nC * nC; ++p) {
+        for (const auto& pr : dir[p]) { out.eka.push_back(pr.first); out.ekb.push_back(pr.second); }
+        out.eap.push_back((int32_t)out.eka.size());
+        for (const auto& pr : via[p]) { out.el1.push_back(pr.first); out.el2.push_back(pr.second); }
+        out.ebp.push_back((int32_t)out.el1.size());
+    }
+    return true;
+}
+
 }  // namespace phx

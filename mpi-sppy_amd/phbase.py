@@ -340,6 +340,8 @@ class PHBase(SPOpt):
             self.convobject = self.ph_converger(self)
         self.conv = None
         self.trivial_bound = self.Ebound(verbose)
+        # per-scenario Iter0 optima (the outer bounds the trivial bound sums), on the device
+        self._iter0_obj_dev = self._obj.clone()
         if dprogress and self.cylinder_rank == 0:
             print("")
             print("After PH Iteration", self._PHIter)
@@ -541,6 +543,12 @@ class PHBase(SPOpt):
         return Eobj
 
     # ------------------------------------------------------------ accessors
+    @property
+    def _iter0_obj(self):
+        """(S_local,) Iter0 subproblem optima, the reference's outer_bound after Iter0
+        (spopt.py:201-206), in the model's sense."""
+        return self._iter0_obj_dev.cpu().numpy() * (1.0 if self.is_minimizing else -1.0)
+
     def xbar_by_node(self):
         """{node_name: (xbar ndarray, xsqbar ndarray)} (host copy)."""
         xb = self._host("xbar")

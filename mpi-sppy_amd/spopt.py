@@ -13,7 +13,8 @@ passes solver options (``iter0_solver_options`` / ``iterk_solver_options``,
 phbase.py:273-275): keys ``pdhg_max_iters``, ``pdhg_check_every``,
 ``pdhg_restart_max``, ``polish``, ``polish_refine``, ``polish_below``,
 ``kkt_tol``, ``opt_tol``, ``polish_reg``, ``warm_start``, ``ipm_after``,
-``ipm_max_it``, ``ipm_tol``, ``lane_solver``, ``as_rounds``, ``warm_passes``, ``wg_warm``.
+``ipm_max_it``, ``ipm_tol``, ``lane_solver``, ``as_rounds``, ``warm_passes``, ``wg_warm``,
+``sp``, ``sp_rounds``.
 """
 import ctypes
 import inspect
@@ -44,6 +45,8 @@ SOLVER_DEFAULTS = {
     "as_rounds": 4,
     "warm_passes": 1,
     "wg_warm": 16,
+    "sp": 1,
+    "sp_rounds": 16,
 }
 
 OPTIMAL, ITER_LIMIT, NUMERIC_FAIL = 1, 2, 3
@@ -109,6 +112,8 @@ class SPOpt(SPBase):
         so.as_rounds = int(o["as_rounds"])
         so.warm_passes = int(o["warm_passes"])
         so.wg_warm = int(o["wg_warm"])
+        so.sp = int(o["sp"])
+        so.sp_rounds = int(o["sp_rounds"])
         return so
 
     def _set_ph_terms(self):
@@ -184,6 +189,9 @@ class SPOpt(SPBase):
                     "lane_warm_certified": stt.lane_warm_certified,
                     "lane_first_certified": stt.lane_first_certified, "stragglers": stragglers,
                     "wg_certified": stt.wg_certified, "wg_ms": stt.wg_ms,
+                    "sp_certified": stt.sp_certified, "sp_warm_rounds": stt.sp_warm_rounds,
+                    "sp_ipm_its": stt.sp_ipm_its, "sp_cold_rounds": stt.sp_cold_rounds,
+                    "sp_refine": stt.sp_refine, "sp_ms": stt.sp_ms,
                     "wall_s": time.perf_counter() - t0, "not_optimal": n_bad})
         if n_bad and gripe:
             stc = self._status.cpu().numpy()

@@ -98,3 +98,71 @@ def test_netdes_synthetic_batch_gpu(gpu_lib):
     o.W_on, o.prox_on = 1, 1
     o.solve_loop()
     assert rel(ph.nonant_values()[pick], o.xn()) < 1e-6
+
+
+# ---- C5b: network-50-30-H (n = 2,940, m = 1,520, 1,470 nonants) through the sparse
+#      workgroup solver (phx_sp.h) -------------------------------------------------
+INST50 = "network-50-30-H-01"
+HIGHS_LP_50 = 75593.51224584531   # round-1 HiGHS LP value of the 30 shipped scenarios
+
+
+def check_netdes50(lib, device, S, iters, pick, solver=None):
+    """S scenarios of network-50-30-H (the 30 shipped ones when S == 30, else the
+    synthetic workload: shipped k mod 30 with perturbed costs, p = 1/S), `iters` PH
+    iterations.  Every subproblem of every solve is certified; the trivial bound
+    matches the oracle's (HiGHS LP + certified polish) on the sampled scenarios'
+    LPs; the last iteration's subproblems of the sample, re-solved by the oracle
+    (independent sparse interior point + certified active-set polish) from the
+    engine's own W / x-bar, agree to 1e-6 in the nonants and 1e-8 in objective."""
+    names = netdes.scenario_names_creator(S)
+    kw = {"instance": INST50}
+    okw = {}
+    if S != 30:
+        kw["num_scens"] = okw["num_scens"] = S
+    opts = {}
+    if solver:
+        opts = {"iter0_solver_options": dict(solver), "iterk_solver_options": dict(solver)}
+    ph, conv, Eobj, tb = run_engine(netdes.scenario_creator, names, kw, iters, lib=lib, device=device,
+                                    options=opts)
+    assert all(s["not_optimal"] == 0 for s in ph.solve_stats), [s["not_optimal"] for s in ph.solve_stats]
+    o = oph.OraclePH([om.netdes(names[k], INST50, **okw) for k in pick], rho=1.0)
+    o.iter0()
+    # Iter0 objective per sampled scenario (unique LP optimum value)
+    assert rel(ph._iter0_obj[pick], o.obj) < 1e-8
+    if S == 30:
+        assert rel(tb, HIGHS_LP_50) < 1e-9
+    o.W = ph.W_array()[pick].copy()
+    o.xbar = np.tile(ph.xbar_by_node()["ROOT"][0], (len(pick), 1))
+    o.W_on, o.prox_on = 1, 1
+    o.solve_loop()
+    assert rel(ph.nonant_values()[pick], o.xn()) < 1e-6
+    assert rel(ph._host("obj")[pick], o.obj) < 1e-8
+    return ph
+
+
+def test_netdes50_sparse_emu(emu):
+    ph = check_netdes50(emu, "cpu", 30, 3, [0, 7, 19, 29])
+    st = ph.solve_stats
+    assert st[0]["sp_certified"] == 30 and st[0]["sp_ipm_its"] > 0
+    assert all(s["sp_certified"] == 30 and s["sp_ipm_its"] == 0 for s in st[1:])   # warm rounds only
+
+
+def test_sparse_forced_on_small_emu(emu, monkeypatch):
+    """PHX_SP=1 routes a problem the dense solvers serve (netdes-10, sslp-sized) through
+    the sparse solver: same results as the dense path."""
+    monkeypatch.setenv("PHX_SP", "1")
+    ph, o = check_netdes_ph(emu, "cpu", iters=3)
+    assert all(s["sp_certified"] == 10 for s in ph.solve_stats)
+
+
+@pytest.mark.gpu
+def test_netdes50_shipped_gpu(gpu_lib):
+    check_netdes50(gpu_lib, None, 30, 4, list(range(30)))
+
+
+@pytest.mark.gpu
+def test_netdes50_10k_gpu(gpu_lib):
+    """BASELINE configs[4], C5b at full size: 10,000 scenarios, 3 PH iterations."""
+    ph = check_netdes50(gpu_lib, None, 10000, 3, [0, 1, 29, 30, 4999, 9998, 9999])
+    print({k: [s[k] for s in ph.solve_stats] for k in ["sp_certified", "sp_ms", "sp_ipm_its", "sp_warm_rounds",
+                                                       "pdhg_iters", "wall_s"]})
