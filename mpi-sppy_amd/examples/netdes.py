@@ -18,7 +18,8 @@ right of the name (``_get_scenario_ix``, netdes.py:79-87).  A shipped scenario k
 takes its own (d, u, b) and probability p[k] (parse.py:32-45); any other k (the
 synthetic 10k-scenario workload) takes shipped scenario k mod K with
 its flow costs d scaled by 1 + 0.2 (r - 1/2), r ~ RandomState(k).rand(E), and
-probability 1/num_scens.  Varying per scenario: the vubs' u coefficients, the cost
+probability 1/num_scens (only with num_scens given: without it an index k >= K raises
+the reference's ValueError, parse.py:34-37).  Varying per scenario: the vubs' u coefficients, the cost
 vector (d), the bals right-hand sides (b).
 """
 import os
@@ -60,12 +61,15 @@ def _get_scenario_ix(sname):
     return int(sname[i:])
 
 
-def scenario_data(k, instance=DEFAULT_INSTANCE):
-    """(d, u, b, p) of scenario index k (p None for a synthetic scenario)."""
+def scenario_data(k, instance=DEFAULT_INSTANCE, synthetic=False):
+    """(d, u, b, p) of scenario index k (p None for a synthetic scenario).  Indices
+    beyond the instance's K scenarios exist only in the synthetic workload
+    (``synthetic``, i.e. num_scens given); otherwise they raise the reference's
+    ValueError (parse.py:34-37)."""
     z = data(instance)
     K = len(z["p"])
-    if k < 0:
-        raise ValueError("Provided scenario index (%d) could not be found (%d total scenarios)" % (k, K))
+    if k < 0 or (k >= K and not synthetic):
+        raise ValueError("Provided scenario index ({}) could not be found ({} total scenarios)".format(k, K))
     if k < K:
         return z["d"][k], z["u"][k], z["b"][k], float(z["p"][k])
     r = np.random.RandomState(k).rand(len(z["c"]))
@@ -77,7 +81,7 @@ def scenario_creator(scenario_name, path=None, instance=None, num_scens=None):
     inst = _instance(path, instance)
     z = data(inst)
     k = _get_scenario_ix(scenario_name)
-    d, u, b, p = scenario_data(k, inst)
+    d, u, b, p = scenario_data(k, inst, synthetic=num_scens is not None)
     edges = [(int(i), int(j)) for i, j in z["edges"]]
     m = lm.LinearModel(scenario_name)
     x = m.add_indexed_var("x", edges, lb=0.0, ub=1.0)
@@ -129,7 +133,7 @@ def batch_creator(scenario_names, path=None, instance=None, num_scens=None):
     bal_vals = np.concatenate(row_sign) if row_sign else np.zeros(0)
     prob = []
     for s, nm in enumerate(scenario_names):
-        d, u, b, p = scenario_data(_get_scenario_ix(nm), inst)
+        d, u, b, p = scenario_data(_get_scenario_ix(nm), inst, synthetic=num_scens is not None)
         A[s, 0:2 * E:2] = -u
         A[s, 1:2 * E:2] = 1.0
         A[s, 2 * E:] = bal_vals

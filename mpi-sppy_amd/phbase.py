@@ -305,6 +305,9 @@ class PHBase(SPOpt):
         """phbase.py:758-872."""
         if self.extensions is not None:
             self.extobject.pre_iter0()
+        # fixedness / values as the extensions left them (phbase.py:788): what
+        # post_solve_bound restores (_restore_original_fixedness)
+        self._save_original_nonants()
         verbose = self.options["verbose"]
         dprogress = self.options["display_progress"]
         dtiming = self.options["display_timing"]

@@ -269,6 +269,11 @@ class SPBase:
         # internal problems are minimisations; max problems are negated (see spopt)
         sgn = 1.0 if self.is_minimizing else -1.0
         c = b.c * sgn
+        # the objective constant (c0, e.g. a Pyomo expression's constant term) is not
+        # part of the device problem: it is added where objectives are read out
+        # (_host obj/outer, Eobjective, Ebound, objs_dict), in the internal min sense
+        self._c0_int = np.asarray(b.c0, dtype=np.float64) * sgn
+        self._pc0 = math.fsum(float(p) * float(v) for p, v in zip(b.prob, self._c0_int))
         d = {}
         d["rowptr"] = self._t(b.rowptr, i32)
         d["colidx"] = self._t(b.colidx, i32)
@@ -386,9 +391,9 @@ class SPBase:
             elif key == "xsqbar":
                 a = self._xsqbar_node.cpu().numpy()
             elif key == "obj":
-                a = self._obj.cpu().numpy() * (1.0 if self.is_minimizing else -1.0)
+                a = (self._obj.cpu().numpy() + self._c0_int) * (1.0 if self.is_minimizing else -1.0)
             elif key == "outer":
-                a = self._outer.cpu().numpy() * (1.0 if self.is_minimizing else -1.0)
+                a = (self._outer.cpu().numpy() + self._c0_int) * (1.0 if self.is_minimizing else -1.0)
             elif key == "status":
                 a = self._status.cpu().numpy()
             else:

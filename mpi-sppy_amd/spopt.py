@@ -240,7 +240,7 @@ class SPOpt(SPBase):
         """sum_s p_s * objective_s incl. active W/prox terms (spopt.py:310-343)."""
         self._objective_now()
         buf = self._expect(self._obj_eval).clone()
-        g = self.mpicomm.allreduce_(buf[0:1].clone())
+        g = self.mpicomm.allreduce_(buf[0:1] + self._pc0)
         v = float(g.item())
         return v if self.is_minimizing else -v
 
@@ -257,7 +257,7 @@ class SPOpt(SPBase):
     def Ebound(self, verbose=False, extra_sum_terms=None):
         """sum_s p_s * outer_bound_s (+ extra terms), spopt.py:346-391."""
         buf = self._expect(self._outer)
-        loc = [float(buf[0].item())]
+        loc = [float(buf[0].item()) + self._pc0]
         if extra_sum_terms is not None:
             loc += list(extra_sum_terms)
         t = torch.tensor(loc, dtype=torch.float64, device=self.device)

@@ -56,7 +56,7 @@ class Xhat_Eval(SPOpt):
     def _fill_objs_dict(self):
         self._objective_now()
         sgn = 1.0 if self.is_minimizing else -1.0
-        vals = self._obj_eval.cpu().numpy() * sgn
+        vals = (self._obj_eval.cpu().numpy() + self._c0_int) * sgn
         self.objs_dict = {k: float(vals[s]) for s, k in enumerate(self.local_scenario_names)}
 
     def Eobjective(self, verbose=False, fct=None):

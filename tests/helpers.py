@@ -33,3 +33,17 @@ REF_XBAR = np.array([96.88717449844287, 274.2239371483933, 128.88888831920772])
 REF_W = np.array([[-16.10425295139681, 70.84705093609978, -54.742797934166234],
                   [-41.104251445950844, 89.57647412029155, -48.47222265026873],
                   [57.20850439734766, -160.42352505639107, 103.21502058443501]])
+
+
+def oracle_continue_from(ph_iter0, scens, iters, rho=1.0):
+    """The oracle's PH iterations 1..iters started from the engine's Iter0 point
+    (degenerate Iter0 LPs may have several optimal vertices; from iteration 1 on the
+    prox term makes each subproblem's nonant optimum unique, so the trajectories must
+    agree).  ph_iter0: an engine run with PHIterLimit = 0."""
+    o = oph.OraclePH(scens, rho=rho)
+    x = ph_iter0._host("x")
+    for k in range(len(scens)):
+        o.x[k] = x[:, k].copy()
+    o.W_on = o.prox_on = 1
+    o.iterk(iters, 1e-10)
+    return o

@@ -160,3 +160,26 @@ def test_post_solve_bound_is_lower_bound(emu):
     ef, _, _ = oph.solve_ef([om.farmer("scen%d" % i, num_scens=6) for i in range(6)])
     assert lb <= ef + 1e-6 * abs(ef)
     assert tb <= lb + 1e-6 * abs(ef)
+
+
+def test_objective_constant_emu(emu):
+    """A scenario objective with a constant term c0: Eobjective, Ebound,
+    the trivial bound and the per-scenario objectives include it (spopt.py:310-391)."""
+    from mpisppy_amd.examples import farmer
+
+    def creator(name, **kw):
+        m = farmer.scenario_creator(name, **kw)
+        m._obj.const += 1000.0 + 10.0 * int(name[4:])
+        return m
+
+    names = farmer.scenario_names_creator(3)
+    base = PH(ph_options(3), names, farmer.scenario_creator, scenario_creator_kwargs={"num_scens": 3},
+              _native_lib=emu, _device="cpu")
+    conv0, E0, tb0 = base.ph_main()
+    ph = PH(dict(ph_options(3), per_scenario_models=True), names, creator, scenario_creator_kwargs={"num_scens": 3},
+            _native_lib=emu, _device="cpu")
+    conv1, E1, tb1 = ph.ph_main()
+    shift = sum((1000.0 + 10.0 * k) / 3.0 for k in range(3))
+    assert abs((E1 - E0) - shift) < 1e-9 * abs(E0) and abs((tb1 - tb0) - shift) < 1e-9 * abs(tb0)
+    assert np.allclose(ph._host("obj") - base._host("obj"), [1000.0, 1010.0, 1020.0])
+    assert conv1 == conv0

@@ -19,23 +19,33 @@ MIP_OPT = 27523.7          # examples/netdes/solutions.dat, network-10-10-H-01 b
 
 
 def test_netdes_batch_equals_models():
-    names = netdes.scenario_names_creator(12)       # Scenario0..9 shipped, 10..11 synthetic
+    names = netdes.scenario_names_creator(10)       # the shipped scenarios, shipped probabilities
     a = from_models(names, [netdes.scenario_creator(nm, path="data/%s.dat" % INST) for nm in names]).compress()
     b = netdes.batch_creator(names, instance=INST).compress()
     for k in ["rowptr", "colidx", "kvar", "Aconst", "Avar", "c", "lb", "ub", "bl", "bu"]:
         assert np.array_equal(getattr(a, k), getattr(b, k)), k
     assert (a.n, a.m) == (108, 64) and a.nnz == b.nnz == 2 * 54 + 2 * 54
     assert list(a.nonant.slot_col) == list(range(54)) and a.rhs_vary and a.c_vary
-    assert a.prob == b.prob and abs(sum(a.prob[:10]) - 1.0) < 1e-12 and a.prob[10] is None
+    assert a.prob == b.prob and abs(sum(a.prob) - 1.0) < 1e-12
+    names = netdes.scenario_names_creator(12)       # 10..11 synthetic: only with num_scens
+    a = from_models(names, [netdes.scenario_creator(nm, instance=INST, num_scens=12) for nm in names]).compress()
+    b = netdes.batch_creator(names, instance=INST, num_scens=12).compress()
+    for k in ["Avar", "c", "bl", "bu"]:
+        assert np.array_equal(getattr(a, k), getattr(b, k)), k
+    assert a.prob == b.prob == [1 / 12] * 12
+    with pytest.raises(ValueError):                 # parse.py:34-37
+        netdes.scenario_creator("Scenario10", instance=INST)
+    with pytest.raises(ValueError):
+        netdes.batch_creator(names, instance=INST)
     with pytest.raises(RuntimeError):
         netdes.scenario_creator("Scenario0")
     assert netdes._get_scenario_ix("Scen07") == 7
 
 
 def test_netdes_oracle_model_matches_creator():
-    for nm in ["Scenario3", "Scenario17"]:
-        sf = netdes.scenario_creator(nm, instance=INST).standard_form()
-        o = om.netdes(nm, INST)
+    for nm, ns in [("Scenario3", None), ("Scenario17", 20)]:
+        sf = netdes.scenario_creator(nm, instance=INST, num_scens=ns).standard_form()
+        o = om.netdes(nm, INST, num_scens=ns)
         A = np.zeros((len(sf["bl"]), len(sf["c"])))
         for i in range(len(sf["bl"])):
             for k in range(sf["rowptr"][i], sf["rowptr"][i + 1]):

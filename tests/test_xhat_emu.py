@@ -156,10 +156,40 @@ def test_post_solve_bound_restores_original_fixedness_emu(emu):
             _native_lib=emu, _device="cpu")
     ph.ph_main()
     W = ph.W_array()
-    ph._save_original_nonants()
     ph._fix_nonants({"ROOT": [100.0, 200.0, 200.0]})
     bound = ph.post_solve_bound()
     o = oph.OraclePH([om.farmer(n, num_scens=6) for n in names], rho=1.0)
+    o.W = W.copy()
+    o.W_on, o.prox_on = 1, 0
+    o.solve_loop()
+    assert rel(bound, o.Ebound()) < 1e-9
+
+
+def test_fixed_in_pre_iter0_stay_fixed_in_post_solve_bound_emu(emu):
+    """Iter0 saves the original nonants after pre_iter0 (phbase.py:788): nonants an
+    extension fixes there are part of the original fixedness, so post_solve_bound
+    (which restores it, phbase.py:473-474) keeps them fixed."""
+    from mpisppy_amd.extensions.extension import Extension
+    fixed = [120.0, 250.0, 130.0]
+
+    class FixRoot(Extension):
+        def pre_iter0(self):
+            self.opt._fix_nonants({"ROOT": fixed})
+
+    names = farmer.scenario_names_creator(3)
+    ph = PH(ph_options(2), names, farmer.scenario_creator, scenario_creator_kwargs={"num_scens": 3},
+            extensions=FixRoot, _native_lib=emu, _device="cpu")
+    ph.ph_main()
+    assert ph.original_fixedness.all()
+    W = ph.W_array()
+    bound = ph.post_solve_bound()
+    assert np.allclose(ph.nonant_values(), np.tile(fixed, (3, 1)))
+    scens = [om.farmer(n, num_scens=3) for n in names]
+    for sc in scens:
+        for (_, _, _, vl) in sc.nodes:
+            for i, v in enumerate(vl):
+                sc.lb[v] = sc.ub[v] = fixed[i]
+    o = oph.OraclePH(scens, rho=1.0)
     o.W = W.copy()
     o.W_on, o.prox_on = 1, 0
     o.solve_loop()
