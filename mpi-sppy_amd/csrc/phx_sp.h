@@ -174,9 +174,15 @@ PHX_HD void sp_reduce(double* v, double* red, int op) {
 // ---------------------------------------------------------------------------
 // Factorization of M for column weights L.hv (0: column eliminated) and row
 // diagonals G.rdg (< 0: inactive row).  Returns false (uniformly) when the
-// separator Schur complement is not positive definite.
+// separator Schur complement is not positive definite.  ipm_safe (interior
+// point): a pivot that collapses relative to the separator row's diagonal of
+// M itself (a dependent row of A H^-1 A' near an interior-point optimum; the
+// B-row elimination cancels up to 1/reg ~ 1e10) is replaced by a huge value,
+// which zeroes that component of the solve — cholesky_ipm's safeguard
+// (phx_lane.h).
 // ---------------------------------------------------------------------------
-PHX_HD bool sp_factor(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds& L, int s) {
+PHX_HD bool sp_factor(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds& L, int s,
+                      bool ipm_safe = false) {
     const int m = P.m, nC = Y.nC, ld = Y.ld;
     // B-row diagonal and the links M_bc
     for (int i = SP_TID; i < m; i += SP_NT) {
@@ -210,12 +216,14 @@ PHX_HD bool sp_factor(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds
         double v;
         if (d1 < 0.0 || d2 < 0.0) {
             v = (c1 == c2) ? 1.0 : 0.0;
+            if (c1 == c2) L.cv[c1] = 1.0;
         } else {
             v = (c1 == c2) ? d1 : 0.0;
             for (int t = Y.eap[p]; t < Y.eap[p + 1]; ++t) {
                 const int ka = Y.eka[t];
                 v += sp_a(P, Y, ka, s) * sp_a(P, Y, Y.ekb[t], s) * L.hv[P.colidx[ka]];
             }
+            if (c1 == c2) L.cv[c1] = v;      // M_cc: the reference of the pivot safeguard
             for (int t = Y.ebp[p]; t < Y.ebp[p + 1]; ++t) {
                 const int l1 = Y.el1[t];
                 v -= L.lv[l1] * L.lv[Y.el2[t]] / L.Mbb[Y.lrow[l1]];
@@ -227,7 +235,12 @@ PHX_HD bool sp_factor(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds
     // right-looking Cholesky, every trailing entry its own work item; L[i][k]
     // (i > k) is stored transposed at Sm[k*ld + i], 1/L_kk in dg
     for (int jj = 0; jj < nC; ++jj) {
-        const double d = L.Sm[jj * ld + jj];
+        double d = L.Sm[jj * ld + jj];
+        if (ipm_safe) {
+            const double d0 = L.cv[jj];
+            if (!(d0 > 0.0 && d0 < 1e300)) return false;
+            if (!(d > 1e-13 * d0)) d = 1e128;
+        }
         if (!(d > 0.0)) return false;
         const double sd = sqrt(d), id = 1.0 / d;
         const int R = nC - jj - 1;
@@ -550,7 +563,7 @@ PHX_HD double sp_ipm(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds&
             G.rdg[i] = dg;
         }
         SP_SYNC();
-        if (!sp_factor(P, Y, G, L, s)) break;
+        if (!sp_factor(P, Y, G, L, s, true)) break;
         // ---- predictor ----
         for (int j = SP_TID; j < n; j += SP_NT) {
             const double l = G.lb[j], u = G.ub[j], x = L.xv[j];

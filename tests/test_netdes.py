@@ -157,12 +157,17 @@ def test_netdes50_sparse_emu(emu):
     assert all(s["sp_certified"] == 30 and s["sp_ipm_its"] == 0 for s in st[1:])   # warm rounds only
 
 
-def test_sparse_forced_on_small_emu(emu, monkeypatch):
-    """PHX_SP=1 routes a problem the dense solvers serve (netdes-10, sslp-sized) through
-    the sparse solver: same results as the dense path."""
-    monkeypatch.setenv("PHX_SP", "1")
+def test_sparse_alone_and_dense_paths_emu(emu, monkeypatch):
+    """netdes-10 (n = 108: beyond the lane solver) through the sparse solver alone
+    (PHX_NO_WG=1: no dense workgroup warm pass) and through the dense generic path
+    (PHX_SP=0: PDHG + dense polish / IPM, the round-1 path): both match the oracle."""
+    monkeypatch.setenv("PHX_NO_WG", "1")
     ph, o = check_netdes_ph(emu, "cpu", iters=3)
     assert all(s["sp_certified"] == 10 for s in ph.solve_stats)
+    monkeypatch.delenv("PHX_NO_WG")
+    monkeypatch.setenv("PHX_SP", "0")
+    ph, o = check_netdes_ph(emu, "cpu", iters=2)
+    assert all(s["sp_certified"] == 0 for s in ph.solve_stats)
 
 
 @pytest.mark.gpu
