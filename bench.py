@@ -1,29 +1,34 @@
-"""bench.py — PH scenario-iterations/s on farmer (BASELINE.json metric).
+"""bench.py — PH scenario-iterations/s + time to conv < 1e-4 (BASELINE.json metric).
 
 A "step" is one PH iteration over every scenario (Compute_Xbar -> Update_W ->
-convergence_diff -> batched subproblem solve), i.e. the body of
-``PHBase.iterk_loop`` (mpisppy/phbase.py:901-970); the timed region is
-``iterk_loop`` itself running K iterations (on the device: phx_iterk).  Workload: farmer,
-crops_multiplier 1, 100,000 synthetic scenarios (configs[2] of BASELINE.json;
-the metric is quoted on it and it fits one MI355X), rho = 1, scenarios sharded
-contiguously over the ranks (strong scaling: the 100k total is fixed).
+convergence_diff -> batched subproblem solve), the body of ``PHBase.iterk_loop``
+(mpisppy/phbase.py:901-970).  Headline workload: farmer, crops_multiplier 1,
+100,000 synthetic scenarios (BASELINE configs[2]; the metric is quoted on it and
+it fits one MI355X), rho = 1, scenarios sharded contiguously over the ranks
+(strong scaling: the 100k total is fixed).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--scens S] [--cm C]
+    python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
 
-Timed region: iterk_loop with PHIterLimit = K bracketed by barrier + device
-synchronize; the MAX over ranks is reported.  Iter0 and W warmup iterations are
-untimed.  --host-loop drives the iterations from Python instead.  Inputs are
-resident in HBM before timing.  Extra keys:
-  roofline      the dominant kernel of the timed region (the structure-
-                specialised lane solver ``phx_lane_warm`` with the lane solver
-                on, the PDHG chunk ``k_chunk`` otherwise): algorithmic bytes
-                 / its average duration from HIP events recorded
-                around it on the solve stream (every --timing-every-th iteration).
-  cpu_baseline  the CPU restatement of the reference PH (oracle/cpu_bench.py:
-                numpy + scipy-HiGHS + polish, one worker process per core) on a
-                bounded sample, run as a child process on rank 0 at N = 1.
-  conv_time     (--conv) wall time from Iter0 to conv < 1e-4.
+Metric: value = S (K + 1) / T, T = wall time of Iter0 + K PH
+iterations (PHBase.Iter0 then PHBase.iterk_loop with PHIterLimit = K, on the
+device: phx_iterk), bracketed by barrier + device synchronize, MAX over ranks; K
+steps are timed, Iter0 counts as one more scenario-solve pass.  W warmup: a full
+untimed Iter0 + W iterations on a separate PH object first (JIT, allocator).
+Inputs resident in HBM before timing.  Extra keys:
+  steady        S K / T_iterk (Iter0 excluded) and the per-iteration time
+  conv_time     wall time from Iter0 to conv < 1e-4 (convthresh 1e-4), iterations
+  roofline      the dominant kernel of the timed iterations (phx_lane_warm):
+                algorithmic bytes / its average duration from HIP
+                events recorded around it on the solve stream (sampled iterations)
+  cpu_baseline  the oracle's CPU restatement of the reference PH (oracle/cpu_bench.py,
+                one worker process per core) on a bounded sample, child process,
+                rank 0 at N = 1
+  configs       (N = 1) the other BASELINE configs, each timed the same way
+                (Iter0 + K' iterations): C2 farmer crops_multiplier=10 x 1,000,
+                C4 aircond 10x10x10, C5a sslp_15_45 x 10,000, C5b netdes
+                network-50-30-H x 10,000 — value, steady state, dominant kernel
+                + roofline, CPU baseline
 """
 import argparse
 import json
@@ -50,38 +55,30 @@ def parse():
     ap.add_argument("--scens", type=int, default=100000)
     ap.add_argument("--cm", type=int, default=1)
     ap.add_argument("--rho", type=float, default=1.0)
-    ap.add_argument("--check-every", type=int, default=64)
-    ap.add_argument("--ipm-after", type=int, default=None, help="PDHG iterations before the IPM finisher")
     ap.add_argument("--lane-solver", type=int, default=1, help="1: structure-specialised lane solver first")
-    ap.add_argument("--as-rounds", type=int, default=None, help="active-set rounds (0: no warm active set)")
+    ap.add_argument("--depth", type=int, default=4, help="phx_iterk: iterations kept enqueued ahead")
+    ap.add_argument("--fused", type=int, default=1, help="phx_iterk: one launch per PH iteration")
+    ap.add_argument("--timing-every", type=int, default=5,
+                    help="phx_iterk: HIP events around the lane kernel of every T-th iteration")
+    ap.add_argument("--no-conv", action="store_true", help="skip time to conv < 1e-4")
+    ap.add_argument("--conv-max-iters", type=int, default=10000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-scens", type=int, default=40000)
     ap.add_argument("--cpu-iters", type=int, default=6)
     ap.add_argument("--cpu-procs", type=int, default=16, help="worker processes (the GPU box's CPU share)")
-    ap.add_argument("--host-loop", action="store_true", help="drive each PH iteration from Python")
-    ap.add_argument("--depth", type=int, default=4, help="phx_iterk: iterations kept enqueued ahead")
-    ap.add_argument("--fused", type=int, default=1,
-                    help="phx_iterk: one phx_lane_warm launch per PH iteration (Update_W + conv + solve + "
-                         "next x-bar partials fused); 0: k_xbar, k_update_w_seg, warm, cold per iteration")
-    ap.add_argument("--timing-every", type=int, default=5,
-                    help="phx_iterk: HIP events around the lane kernel of every T-th iteration")
-    ap.add_argument("--conv", action="store_true", help="also measure time to conv < 1e-4")
-    ap.add_argument("--conv-max-iters", type=int, default=5000)
+    ap.add_argument("--configs", default="all", help="'all', 'none' or a comma list of C2,C4,C5a,C5b")
+    ap.add_argument("--config-steps", type=int, default=10, help="K' of the other configs")
+    ap.add_argument("--only", default=None, help="run one config as the headline (C2, C4, C5a, C5b)")
     return ap.parse_args()
 
 
+# ---------------------------------------------------------------- algorithmic bytes
 def lane_bytes(b, fused=False):
-    """Algorithmic HBM bytes of phx_lane_warm per scenario.
-
-    reads : varying A values, W and rho of the nonant slots with their x-bar
-            index (x-bar itself is a per-node vector, cache-resident), the
-            active-set words, plus c / bounds / row bounds where they vary
-    writes: x (n), row duals y (m), objective, status + iteration count
-            (caller's and the context's), flags, active-set words
-    The scenario-invariant data are literals of the JIT-specialised kernel.
-    fused (phx_iterk fused mode): + the previous solve's nonant x and the
-    prob_coeff (Update_W / next x-bar partials), + the W write-back.
-    """
+    """phx_lane_warm per scenario solve.  reads: varying A values, W
+    and rho of the nonant slots with their x-bar index, the active-set words, plus
+    c / bounds / row bounds where they vary; writes: x (n), row duals (m),
+    objective, status + iteration count, flags, active-set words.  fused: + the
+    previous nonant x and prob_coeff (Update_W / next x-bar), + the W write-back."""
     nw = (2 * (b.n + b.m) + 31) // 32
     rd = 8 * (b.nvar + 2 * b.nonant.N) + 4 * b.nonant.N + 4 * nw
     rd += 8 * b.n * int(b.c_vary) + 16 * b.n * int(b.bnd_vary) + 16 * b.m * int(b.rhs_vary)
@@ -92,45 +89,176 @@ def lane_bytes(b, fused=False):
     return rd + wr
 
 
-def pdhg_bytes(b):
-    """Algorithmic bytes of one PDHG iteration of one scenario in k_chunk:
-    the SpMM pair with de-duplicated A values
-    8*(2*nnz_var + 2*n + 2*m) plus the fused vector updates 8*(7n + 5m)."""
-    return 8 * (2 * b.nvar + 2 * b.n + 2 * b.m) + 8 * (7 * b.n + 5 * b.m)
-
-
 def wg_bytes(b):
-    """Algorithmic bytes of one scenario solve in k_wg_warm (phx_wg.h): reads
-    the varying A values, qN/pN of the nonant slots and the warm-start point
-    (x n, y m); writes x, x0, xT (3n) and y, y0, yT (3m) plus status + iters."""
+    """k_wg_warm per scenario solve: reads the varying A values, qN/pN of the nonant
+    slots and the warm-start point (x n, y m); writes x, x0, xT (3n) and y, y0, yT
+    (3m) plus status + iters."""
     return 8 * (b.nvar + 2 * b.nonant.N + b.n + b.m) + 8 * (3 * b.n + 3 * b.m) + 8
 
 
-def pmc_traffic(kernel, args):
+def sp_bytes(b):
+    """k_sp_solve per scenario solve (phx_sp.h): reads the varying A values, c / bounds
+    / row bounds where they vary, qN/pN of the nonant slots, the warm-start point
+    (x n, y m); writes the outputs x (n), y (m) and the next warm start x, x0, xT,
+    y, y0, yT, plus objective, status, iterations, flags."""
+    rd = 8 * (b.nvar + 2 * b.nonant.N + b.n + b.m)
+    rd += 8 * b.n * int(b.c_vary) + 16 * b.n * int(b.bnd_vary) + 16 * b.m * int(b.rhs_vary)
+    wr = 8 * 4 * (b.n + b.m) + 8 + 12
+    return rd + wr
+
+
+def pmc_traffic(kernel, tag):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
-    (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; scripts/pmc_summary.py).
-    Counters need their own profiler runs, so they are read from profiles/."""
+    (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; scripts/pmc_summary.py): counters
+    need their own profiler runs, so they are read from profiles/ (newest first)."""
     import glob
-    if args.scens != 100000 or args.cm != 1:
-        return None, None
-    files = sorted(glob.glob(os.path.join(_ROOT, "profiles", "r*_pmc_%s.json" % kernel.replace("phx_", ""))))
+    files = sorted(glob.glob(os.path.join(_ROOT, "profiles", "r*_pmc_%s_%s.json" % (tag, kernel))))
     if not files:
         return None, None
     d = json.load(open(files[-1]))
-    t = d.get("hbm_bytes_per_launch", {}).get("total")
-    return t, os.path.relpath(files[-1], _ROOT)
+    return d.get("hbm_bytes_per_launch", {}).get("total"), os.path.relpath(files[-1], _ROOT)
 
 
-def cpu_baseline(args):
+def cpu_baseline(args, model="farmer", cm=1, scens=None, iters=None, total=None, timeout=900):
     """oracle/cpu_bench.py in a child process (it never touches the GPU)."""
     procs = max(1, min(args.cpu_procs, os.cpu_count() or 1))
-    cmd = [sys.executable, "-m", "oracle.cpu_bench", "--scens", str(args.cpu_scens), "--iters",
-           str(args.cpu_iters), "--procs", str(procs), "--cm", str(args.cm), "--rho", str(args.rho)]
-    r = subprocess.run(cmd, cwd=_ROOT, capture_output=True, text=True, timeout=600)
+    cmd = [sys.executable, "-m", "oracle.cpu_bench", "--model", model, "--scens", str(scens or args.cpu_scens),
+           "--iters", str(iters or args.cpu_iters), "--procs", str(procs), "--cm", str(cm), "--rho", str(args.rho)]
+    if total:
+        cmd += ["--scens-total", str(total)]
+    try:
+        r = subprocess.run(cmd, cwd=_ROOT, capture_output=True, text=True, timeout=timeout)
+    except subprocess.TimeoutExpired:
+        return {"error": "timeout"}
     if r.returncode != 0:
         return {"error": r.stderr[-500:]}
     d = json.loads(r.stdout.strip().splitlines()[-1])
     return {k: d[k] for k in ["value", "unit", "cores", "kind", "sample", "seconds"]}
+
+
+# ---------------------------------------------------------------- workloads
+def workloads():
+    from mpisppy_amd.examples import farmer, sslp, netdes, aircond
+    from mpisppy_amd.utils import sputils
+    bfs = [10, 10, 10]
+    return {
+        "C3": dict(creator=farmer.scenario_creator, names=lambda S: farmer.scenario_names_creator(S),
+                   kw=lambda S, cm: {"num_scens": S, "crops_multiplier": cm}, nodes=None,
+                   desc="farmer crops_multiplier=%d, %d scenarios (BASELINE configs[2])"),
+        "C2": dict(creator=farmer.scenario_creator, names=lambda S: farmer.scenario_names_creator(1000),
+                   kw=lambda S, cm: {"num_scens": 1000, "crops_multiplier": 10}, nodes=None, S=1000,
+                   desc="farmer crops_multiplier=10, 1,000 scenarios (BASELINE configs[1])",
+                   cpu=dict(model="farmer", cm=10, scens=256, iters=2, total=1000)),
+        "C4": dict(creator=aircond.scenario_creator, names=lambda S: ["scen%d" % i for i in range(1000)],
+                   kw=lambda S, cm: {"branching_factors": bfs}, S=1000,
+                   nodes=sputils.create_nodenames_from_branching_factors(bfs),
+                   desc="aircond branching 10x10x10, 1,000 scenarios, 111 non-leaf nodes (BASELINE configs[3])",
+                   cpu=None),
+        "C5a": dict(creator=sslp.scenario_creator, names=lambda S: sslp.scenario_names_creator(10000),
+                    kw=lambda S, cm: {"num_scens": 10000}, nodes=None, S=10000,
+                    desc="sslp_15_45 LP relaxation, 10,000 stochastic-RHS scenarios (BASELINE configs[4])",
+                    cpu=dict(model="sslp", scens=128, iters=1, total=10000)),
+        "C5b": dict(creator=netdes.scenario_creator, names=lambda S: netdes.scenario_names_creator(10000),
+                    kw=lambda S, cm: {"instance": "network-50-30-H-01", "num_scens": 10000}, nodes=None, S=10000,
+                    desc="netdes network-50-30-H LP relaxation, 10,000 scenarios (BASELINE configs[4])",
+                    cpu=dict(model="netdes50", scens=32, iters=1, total=10000)),
+    }
+
+
+def make_ph(w, S, cm, rho, so, iters, convthresh=1e-10):
+    from mpisppy_amd.opt.ph import PH
+    opts = {"solver_name": "phx", "PHIterLimit": iters, "defaultPHrho": rho, "convthresh": convthresh,
+            "verbose": False, "display_progress": False, "iter0_solver_options": dict(so),
+            "iterk_solver_options": dict(so)}
+    return PH(opts, w["names"](S), w["creator"], scenario_creator_kwargs=w["kw"](S, cm), all_nodenames=w["nodes"])
+
+
+def timed_run(ph, K):
+    """Iter0 + K PH iterations, bracketed by barrier + synchronize (PH.ph_main without
+    post_loops).  Returns (T, T_iter0, T_iterk), the max over ranks."""
+    ph.PH_Prep()
+    ph.subproblem_creation(False)
+    ph.options["PHIterLimit"] = K
+    ph.mpicomm.Barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ph.Iter0()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    ph.iterk_loop()
+    ph._settle()
+    torch.cuda.synchronize()
+    ph.mpicomm.Barrier()
+    t2 = time.perf_counter()
+    tt = torch.tensor([t2 - t0, t1 - t0, t2 - t1], dtype=torch.float64, device="cuda")
+    ph.mpicomm.allreduce_max_(tt)
+    return [float(v) for v in tt.cpu()]
+
+
+def dominant_kernel(ph, K, fused):
+    """(kernel, avg launch seconds, launches, bytes per unit, units per launch) of the
+    timed iterations' dominant kernel."""
+    b = ph.batch
+    st = getattr(ph, "iterk_stats", None)
+    if st is not None and st.get("warm_launches", 0) > 0:
+        return ("phx_lane_warm", st["lane_warm_ms"] / 1e3 / st["warm_launches"], st["warm_launches"],
+                lane_bytes(b, fused=bool(st.get("fused")) and fused), b.S)
+    stats = ph.solve_stats[-K:]
+    cand = {
+        "phx_lane_warm": (sum(s.get("lane_warm_ms", 0.0) for s in stats), lane_bytes(b)),
+        "k_wg_warm": (sum(s.get("wg_ms", 0.0) for s in stats), wg_bytes(b)),
+        "k_sp_solve": (sum(s.get("sp_ms", 0.0) for s in stats), sp_bytes(b)),
+    }
+    name = max(cand, key=lambda k: cand[k][0])
+    ms, bpu = cand[name]
+    launches = sum(1 for s in stats if s.get({"phx_lane_warm": "lane_warm_ms", "k_wg_warm": "wg_ms",
+                                              "k_sp_solve": "sp_ms"}[name], 0.0) > 0.0)
+    units = b.S
+    if name == "k_sp_solve":
+        # the sparse pass after the dense warm pass sees only the lanes that pass left
+        cert = [s.get("sp_certified", 0) for s in stats if s.get("sp_ms", 0.0) > 0.0]
+        if cert and any(s.get("wg_ms", 0.0) > 0.0 for s in stats):
+            units = max(1, int(np.mean(cert)))
+    return name, ms / 1e3 / max(launches, 1), launches, bpu, units
+
+
+def roofline(kernel, avg_s, launches, bpu, units, traffic=None, traffic_src=None):
+    bytes_per_launch = bpu * units
+    achieved = bytes_per_launch / avg_s / 1e9 if avg_s > 0 else 0.0
+    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/launch",
+            "traffic_source": traffic_src, "algorithmic_bytes_per_launch": bytes_per_launch, "kernel": kernel,
+            "bytes_per_unit": bpu, "unit_def": "scenario solve", "units_per_launch": units,
+            "avg_launch_us": avg_s * 1e6, "launches": launches}
+
+
+def run_config(name, w, args, K, so, world):
+    """One secondary config at N = 1: Iter0 + K iterations on a fresh PH object."""
+    S = w["S"]
+    t = time.perf_counter()
+    ph = make_ph(w, S, 1, args.rho, so, K)
+    torch.cuda.synchronize()
+    setup = time.perf_counter() - t
+    T, T0, Tk = timed_run(ph, K)
+    kernel, avg_s, launches, bpu, units = dominant_kernel(ph, K, True)
+    nbad = sum(s.get("not_optimal", 0) for s in ph.solve_stats)
+    st = getattr(ph, "iterk_stats", None)
+    if st is not None:
+        nbad += st.get("not_optimal", 0)
+    res = {"workload": w["desc"], "scenarios": S, "n": ph.batch.n, "m": ph.batch.m, "nnz": ph.batch.nnz,
+           "nonants": ph.batch.nonant.N, "steps": K,
+           "value": S * (K + 1) / T, "unit": "scenario-iterations/s", "T_s": T, "iter0_s": T0,
+           "steady": {"value": S * K / Tk, "ms_per_step": Tk * 1e3 / K},
+           "roofline": roofline(kernel, avg_s, launches, bpu, units),
+           "solver": ph._native.jit_info(ph._ctx).decode(), "not_optimal": nbad, "setup_s": setup,
+           "loop": "phx_iterk (device-driven)" if st is not None else "PHBase host loop (deferred solves)"}
+    if w.get("cpu") and not args.no_cpu_baseline:
+        c = w["cpu"]
+        res["cpu_baseline"] = cpu_baseline(args, model=c["model"], cm=c.get("cm", 1), scens=c["scens"],
+                                           iters=c["iters"], total=c["total"])
+    del ph
+    torch.cuda.empty_cache()
+    return res
 
 
 def main():
@@ -145,165 +273,65 @@ def main():
     else:
         torch.cuda.set_device(0)
     import mpisppy_amd  # noqa: F401
-    from mpisppy_amd.opt.ph import PH
-    from mpisppy_amd.examples import farmer
-
-    S = args.scens
-    names = farmer.scenario_names_creator(S)
-    solver_opts = {"pdhg_check_every": args.check_every, "lane_solver": args.lane_solver,
-                   "iterk_depth": args.depth, "iterk_timing": args.timing_every, "iterk_fused": args.fused}
-    if args.ipm_after is not None:
-        solver_opts["ipm_after"] = args.ipm_after
-    if args.as_rounds is not None:
-        solver_opts["as_rounds"] = args.as_rounds
-    opts = {"solver_name": "phx", "PHIterLimit": 10 ** 9, "defaultPHrho": args.rho, "convthresh": 1e-10,
-            "verbose": False, "display_progress": False, "iter0_solver_options": dict(solver_opts),
-            "iterk_solver_options": dict(solver_opts)}
-    t_setup = time.perf_counter()
-    ph = PH(opts, names, farmer.scenario_creator,
-            scenario_creator_kwargs={"num_scens": S, "crops_multiplier": args.cm})
-    ph.PH_Prep()
-    ph.subproblem_creation(False)
-    torch.cuda.synchronize()
-    t_setup = time.perf_counter() - t_setup
-
-    def step():
-        ph._PHIter += 1
-        ph.Compute_Xbar(False)
-        ph.Update_W(False)
-        ph.conv = ph.convergence_diff()
-        ph.solve_loop(solver_options=ph.current_solver_options, gripe=False)
-
-    t_iter0 = time.perf_counter()
-    ph.Iter0()
-    torch.cuda.synchronize()
-    t_iter0 = time.perf_counter() - t_iter0
+    W = workloads()
     K = args.steps
+    so = {"lane_solver": args.lane_solver, "iterk_depth": args.depth, "iterk_timing": args.timing_every,
+          "iterk_fused": args.fused}
+    hl = W["C3"] if args.only is None else W[args.only]
+    S = args.scens if args.only is None else hl["S"]
+    cm = args.cm if args.only is None else 1
+    # ---- warmup: a full untimed Iter0 + W iterations on its own object ----
+    t = time.perf_counter()
+    ph = make_ph(hl, S, cm, args.rho, so, args.warmup)
+    ph.ph_main(finalize=False)
+    torch.cuda.synchronize()
+    t_warm = time.perf_counter() - t
+    del ph
+    # ---- timed: Iter0 + K iterations on a fresh object ----
+    t = time.perf_counter()
+    ph = make_ph(hl, S, cm, args.rho, so, K)
+    torch.cuda.synchronize()
+    t_setup = time.perf_counter() - t
+    T, T0, Tk = timed_run(ph, K)
+    st = getattr(ph, "iterk_stats", None)
+    if st is not None and (st["iters"] != K or st["solves"] != K):
+        raise RuntimeError("timed iterk_loop did not run %d full iterations: %s" % (K, st))
+    kernel, avg_s, launches, bpu, units = dominant_kernel(ph, K, args.fused)
     b = ph.batch
-    if args.host_loop or not ph._native_loop_ok():
-        # one PHBase method call after the other from Python (the reference's loop body)
-        for _ in range(args.warmup):
-            step()
-        ph._settle()
-        n0 = len(ph.solve_stats)
-        ph.mpicomm.Barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(K):
-            step()
-        ph._settle()             # the last solve may be deferred: finish it inside the timed region
-        torch.cuda.synchronize()
-        ph.mpicomm.Barrier()
-        dt = time.perf_counter() - t0
-        stats = ph.solve_stats[n0:]
-        lane_warm_ms = sum(s.get("lane_warm_ms", 0.0) for s in stats)
-        warm_launches = sum(1 for s in stats if s.get("lane_warm_ms", 0.0) > 0.0)
-        loop_info = {"loop": "host (PHBase methods per iteration, deferred solves)"}
-        fused_ran = False
-    else:
-        # PHBase.iterk_loop itself: with no per-iteration hooks it runs on the
-        # device (phx_iterk: pipelined iterations, device-side stop test)
-        ph.options["PHIterLimit"] = args.warmup
-        ph.iterk_loop()
-        torch.cuda.synchronize()
-        ph.options["PHIterLimit"] = K
-        ph.mpicomm.Barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        ph.iterk_loop()
-        torch.cuda.synchronize()
-        ph.mpicomm.Barrier()
-        dt = time.perf_counter() - t0
-        st = getattr(ph, "iterk_stats", None)
-        if st is None or st["iters"] != K or st["solves"] != K:
-            raise RuntimeError("timed iterk_loop did not run %d full iterations: %s" % (K, st))
-        stats = []
-        lane_warm_ms = st["lane_warm_ms"]
-        warm_launches = st["warm_launches"]
-        fused_ran = bool(st.get("fused", False))
-        loop_info = {"loop": "PHBase.iterk_loop -> phx_iterk (device-driven, depth %d%s)"
-                             % (args.depth, ", fused: one launch per PH iteration" if fused_ran else ""),
-                     "straggler_stops": st["straggler_stops"], "stragglers": st["stragglers"],
-                     "not_optimal": st["not_optimal"]}
-    dt_t = torch.tensor([dt], dtype=torch.float64, device="cuda")
-    ph.mpicomm.allreduce_max_(dt_t)
-    dt = float(dt_t.item())
-    lane_on = lane_warm_ms > 0.0
-    if lane_on:
-        # dominant kernel: the warm active-set lane kernel, one launch per step over all local scenarios
-        k_ms = lane_warm_ms
-        launches = warm_launches
-        bpu = lane_bytes(b, fused=fused_ran)
-        units_per_launch = b.S
-        kernel = "phx_lane_warm"
-    elif sum(s.get("wg_ms", 0.0) for s in stats) > 0.0:
-        # generic path with the workgroup warm active-set pass (medium subproblems)
-        k_ms = sum(s.get("wg_ms", 0.0) for s in stats)
-        launches = sum(1 for s in stats if s.get("wg_ms", 0.0) > 0.0)
-        bpu = wg_bytes(b)
-        units_per_launch = b.S
-        kernel = "k_wg_warm"
-    else:
-        k_ms = sum(s["pdhg_ms"] for s in stats)
-        launches = sum(s["launches"] for s in stats)
-        bpu = pdhg_bytes(b)
-        units_per_launch = sum(s["lane_iters"] for s in stats) / max(launches, 1)
-        kernel = "k_chunk"
-    avg_launch_s = k_ms / 1e3 / max(launches, 1)
-    bytes_per_launch = bpu * units_per_launch
-    achieved = bytes_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
-    value = S * K / dt
-    traffic, traffic_src = pmc_traffic(kernel, args) if world == 1 else (None, None)
+    traffic, tsrc = (pmc_traffic(kernel, "farmer100k") if world == 1 and args.only is None and S == 100000
+                     and cm == 1 else (None, None))
+    nbad = sum(s.get("not_optimal", 0) for s in ph.solve_stats) + (st.get("not_optimal", 0) if st else 0)
     res = {
-        "metric": "PH scenario-iterations/sec (farmer)",
-        "value": value,
+        "metric": "PH scenario-iterations/sec (farmer 100k) + time to conv<1e-4",
+        "value": S * (K + 1) / T,
         "unit": "scenario-iterations/s",
         "n_gpus": world,
         "steps": K,
         "warmup": args.warmup,
-        "ms_per_step": dt * 1e3 / K,
+        "ms_per_step": T * 1e3 / (K + 1),
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (farmer scenario generator, RandomState-seeded yields as the reference)",
-        "config": {"workload": "farmer crops_multiplier=%d, %d scenarios, rho=%g, PH iterate" % (args.cm, S, args.rho),
+        "data": "synthetic (the reference's scenario generators restated: RandomState-seeded yields etc.)",
+        "config": {"workload": (hl["desc"] % (cm, S)) if args.only is None else hl["desc"],
                    "scenarios": S, "scenarios_per_gpu": b.S, "n": b.n, "m": b.m, "nnz": b.nnz,
-                   "nnz_varying": b.nvar, "nonants": b.nonant.N,
+                   "nnz_varying": b.nvar, "nonants": b.nonant.N, "rho": args.rho,
+                   "timed": "Iter0 + K PH iterations (value = S(K+1)/T, SURVEY §8(d))",
                    "parallelism": "scenario-sharded x%d, RCCL allreduce" % world},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/launch",
-                     "traffic_source": traffic_src, "algorithmic_bytes_per_launch": bytes_per_launch,
-                     "kernel": kernel, "bytes_per_unit": bpu,
-                     "unit_def": "scenario PDHG iteration" if kernel == "k_chunk" else "scenario solve",
-                     "units_per_launch": units_per_launch,
-                     "avg_launch_us": avg_launch_s * 1e6, "launches": launches},
-        "loop": loop_info,
-        # lane_warm: average sampled launch (one launch per step)
-        "kernel_ms_per_step": {"lane_warm": lane_warm_ms / max(warm_launches, 1) if not stats else lane_warm_ms / K,
-                               "lane_warm_list": sum(s.get("lane_warm_list_ms", 0.0) for s in stats) / K,
-                               "lane_cold": sum(s.get("lane_ms", 0.0) for s in stats) / K,
-                               "pdhg": sum(s["pdhg_ms"] for s in stats) / K,
-                               "polish": sum(s["polish_ms"] for s in stats) / K,
-                               "ipm": sum(s["ipm_ms"] for s in stats) / K,
-                               "wg_warm": sum(s.get("wg_ms", 0.0) for s in stats) / K},
-        "wg_certified_per_step": [s.get("wg_certified") for s in stats],
-        "lane_certified_per_step": [s.get("lane_certified") for s in stats],
-        "lane_warm_certified_per_step": [s.get("lane_warm_certified") for s in stats],
-        "lane_first_certified_per_step": [s.get("lane_first_certified") for s in stats],
-        "pdhg_iters_per_step": [s["pdhg_iters"] for s in stats],
-        "solver_options": solver_opts,
-        "not_optimal": sum(s["not_optimal"] for s in stats) if stats else loop_info.get("not_optimal"),
-        "setup_s": t_setup, "iter0_s": t_iter0,
+        "T_s": T, "iter0_s": T0,
+        "steady": {"value": S * K / Tk, "ms_per_step": Tk * 1e3 / K, "def": "S K / T_iterk (Iter0 excluded)"},
+        "roofline": roofline(kernel, avg_s, launches, bpu, units, traffic, tsrc),
+        "loop": ("PHBase.iterk_loop -> phx_iterk (device-driven, depth %d%s)"
+                 % (args.depth, ", fused" if st and st.get("fused") else "")) if st else "PHBase host loop",
+        "not_optimal": nbad, "setup_s": t_setup, "warmup_s": t_warm,
+        "solver": ph._native.jit_info(ph._ctx).decode(),
     }
-    if args.conv:
-        # time to conv < 1e-4 from Iter0 (fresh object, same data)
-        del ph
-        opts2 = dict(opts)
-        opts2["convthresh"] = 1e-4
-        opts2["PHIterLimit"] = args.conv_max_iters
-        ph2 = PH(opts2, names, farmer.scenario_creator,
-                 scenario_creator_kwargs={"num_scens": S, "crops_multiplier": args.cm})
+    del ph
+    torch.cuda.empty_cache()
+    # ---- time to conv < 1e-4 from Iter0 (fresh object, same data) ----
+    if not args.no_conv:
+        ph2 = make_ph(hl, S, cm, args.rho, so, args.conv_max_iters, convthresh=1e-4)
         torch.cuda.synchronize()
         ph2.mpicomm.Barrier()
         t0 = time.perf_counter()
@@ -311,10 +339,22 @@ def main():
         torch.cuda.synchronize()
         tc = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
         ph2.mpicomm.allreduce_max_(tc)
-        res["conv_time"] = {"seconds": float(tc.item()), "iterations": ph2._PHIter,
-                            "conv": ph2.conv, "convthresh": 1e-4}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(args)
+        res["conv_time"] = {"seconds": float(tc.item()), "iterations": ph2._PHIter, "conv": ph2.conv,
+                            "convthresh": 1e-4, "converged": bool(ph2.conv is not None and ph2.conv < 1e-4)}
+        del ph2
+        torch.cuda.empty_cache()
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.only is None:
+        res["cpu_baseline"] = cpu_baseline(args, cm=cm)
+    # ---- the other BASELINE configs (one GPU) ----
+    if world == 1 and args.only is None and args.configs != "none":
+        names = ["C2", "C4", "C5a", "C5b"] if args.configs == "all" else args.configs.split(",")
+        res["configs"] = {}
+        for nm in names:
+            try:
+                res["configs"][nm] = run_config(nm, W[nm], args, min(K, args.config_steps), so, world)
+            except Exception as e:     # reported, never hidden
+                res["configs"][nm] = {"error": repr(e)[:500]}
+            print("[bench] %s done" % nm, file=sys.stderr, flush=True)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

@@ -31,8 +31,27 @@ if _ROOT not in sys.path:
 from oracle import models as om, ph as oph  # noqa: E402
 
 
-def _worker(conn, names, S, cm, rho):
-    scens = [om.farmer(nm, crops_multiplier=cm, num_scens=S) for nm in names]
+def make_scen(model, nm, S, cm=1):
+    """One oracle scenario of the bench workloads (two-stage: one ROOT x-bar)."""
+    if model == "farmer":
+        return om.farmer(nm, crops_multiplier=cm, num_scens=S)
+    if model == "sslp":
+        return om.sslp(nm, num_scens=S)
+    if model == "netdes50":
+        return om.netdes(nm, "network-50-30-H-01", num_scens=S)
+    raise ValueError(model)
+
+
+def names_of(model, S):
+    if model == "farmer":
+        return ["scen%d" % i for i in range(S)]
+    if model == "sslp":
+        return ["Scenario%d" % (i + 1) for i in range(S)]
+    return ["Scenario%d" % i for i in range(S)]
+
+
+def _worker(conn, names, S, cm, rho, model="farmer"):
+    scens = [make_scen(model, nm, S, cm) for nm in names]
     o = oph.OraclePH(scens, rho=rho)
     o.iter0()
     conn.send((o.xn(), o.obj.copy()))
@@ -49,8 +68,11 @@ def _worker(conn, names, S, cm, rho):
     conn.close()
 
 
-def run(S, K, P, cm=1, rho=1.0):
-    names = ["scen%d" % i for i in range(S)]
+def run(S, K, P, cm=1, rho=1.0, model="farmer", S_total=None):
+    """K PH iterations over a sample of S scenarios (probabilities 1/S_total: the
+    subproblems of the full workload; x-bar over the sample)."""
+    St = S_total or S
+    names = names_of(model, S)
     avg = S / P
     slices = [names[int(r * avg):int((r + 1) * avg)] for r in range(P)]
     ctx = mp.get_context("fork")
@@ -58,13 +80,13 @@ def run(S, K, P, cm=1, rho=1.0):
     t_setup = time.perf_counter()
     for sl in slices:
         a, b = ctx.Pipe()
-        p = ctx.Process(target=_worker, args=(b, sl, S, cm, rho))
+        p = ctx.Process(target=_worker, args=(b, sl, St, cm, rho, model))
         p.start()
         pipes.append(a)
         procs.append(p)
     res = [c.recv() for c in pipes]          # Iter0 done everywhere
     t_setup = time.perf_counter() - t_setup
-    prob = 1.0 / S
+    prob = 1.0 / S                           # x-bar over the sample
     xn = np.concatenate([r[0] for r in res])
     t0 = time.perf_counter()
     conv = None
@@ -82,9 +104,10 @@ def run(S, K, P, cm=1, rho=1.0):
         p.join()
     return {"value": S * K / dt, "unit": "scenario-iterations/s", "cores": P, "kind": "port",
             "seconds": dt, "setup_and_iter0_seconds": t_setup, "conv_last": conv,
-            "sample": "oracle PH restatement (numpy + scipy-HiGHS 1.8 LP/QP + KKT polish), farmer cm=%d, %d "
-                      "scenarios x %d PH iterations after Iter0, %d worker processes (contiguous slices, "
-                      "parent = Allreduce)" % (cm, S, K, P)}
+            "sample": "oracle PH restatement (numpy + scipy-HiGHS 1.8 LP/QP or sparse IPM + certified KKT "
+                      "polish), %s, %d scenarios x %d PH iterations after Iter0, %d worker processes "
+                      "(contiguous slices, parent = Allreduce)"
+                      % ("farmer cm=%d" % cm if model == "farmer" else model, S, K, P)}
 
 
 def main():
@@ -94,8 +117,10 @@ def main():
     ap.add_argument("--procs", type=int, default=min(16, os.cpu_count() or 1))
     ap.add_argument("--cm", type=int, default=1)
     ap.add_argument("--rho", type=float, default=1.0)
+    ap.add_argument("--model", default="farmer", choices=["farmer", "sslp", "netdes50"])
+    ap.add_argument("--scens-total", type=int, default=None, help="probability 1/S_total (the full workload)")
     a = ap.parse_args()
-    print(json.dumps(run(a.scens, a.iters, a.procs, a.cm, a.rho)), flush=True)
+    print(json.dumps(run(a.scens, a.iters, a.procs, a.cm, a.rho, a.model, a.scens_total)), flush=True)
 
 
 if __name__ == "__main__":

@@ -60,6 +60,10 @@ def highs_solve(A, bl, bu, lb, ub, q, p=None, want_basis=False):
     h.setOptionValue("output_flag", False)
     h.setOptionValue("primal_feasibility_tolerance", 1e-10)
     h.setOptionValue("dual_feasibility_tolerance", 1e-10)
+    # HiGHS 1.8's active-set QP solver can cycle (sslp prox QPs): bounded, the
+    # caller then falls back to ipm_qp
+    h.setOptionValue("qp_iteration_limit", 20000)
+    h.setOptionValue("time_limit", 20.0)
     lp = _core.HighsLp()
     lp.num_col_ = n
     lp.num_row_ = m
@@ -366,6 +370,16 @@ def solve(A, bl, bu, lb, ub, q, p=None, do_polish=True):
         xp, _, rounds = certified_polish(A, bl, bu, lb, ub, q, p, x, y0=y)
     else:
         x, status, cs, rs = highs_solve(A, bl, bu, lb, ub, q, p, want_basis=True)
+        is_qp = p is not None and np.any(np.asarray(p) != 0)
+        if status != "Optimal" and is_qp and status in ("Iteration limit reached", "Time limit reached"):
+            x, y, ok = ipm_qp(A, bl, bu, lb, ub, q, p)
+            STATS["ipm"] += 1
+            if not ok:
+                return x, False
+            xp, _, rounds = certified_polish(A, bl, bu, lb, ub, q, p, x, y0=y)
+            STATS["solves"] += 1
+            STATS["rounds"] += rounds
+            return xp, True
         if status != "Optimal":
             return x, False
         if not do_polish:
