@@ -256,3 +256,11 @@ def test_farmer_cm10_workgroup_warm_pass(emu):
     oc = oracle_continue_from(ph00, [om.farmer("scen%d" % i, crops_multiplier=10, num_scens=S) for i in range(S)], it)
     assert rel(ph1.W_array(), oc.W) < 1e-6
     assert rel(ph1.xbar_by_node()["ROOT"][0], oc.xbar[0]) < 1e-8
+
+
+def test_time_to_conv_emu(emu):
+    """farmer-3 to conv < 1e-4 through the emulated phx_iterk: the oracle's stop
+    iteration (94) and the reference's converged nonants (test_gpu_parity.py)."""
+    import test_gpu_parity as tg
+    ph = tg.check_time_to_conv(emu, "cpu", 3)
+    assert ph._PHIter == 94
