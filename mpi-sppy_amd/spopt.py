@@ -229,11 +229,18 @@ class SPOpt(SPBase):
 
     # ------------------------------------------------------------ expectations
     def _expect(self, values):
+        """[sum p*values, sum p, sum p*[optimal]] over the local scenarios (device);
+        cached until the next device operation (Iter0 asks three times: E1,
+        feas_prob, Ebound)."""
         self._settle()
+        key = (values.data_ptr(), self._host_epoch)
+        if getattr(self, "_expect_key", None) == key:
+            return self._expect_buf
         lib = self._native
         lib.check(self._ctx, lib.expect(self._ctx, self._prob.data_ptr(), values.data_ptr(),
                                         self._status.data_ptr(), self._expect_buf.data_ptr(),
                                         self._stream()), "expect")
+        self._expect_key = key
         return self._expect_buf
 
     def Eobjective(self, verbose=False):
@@ -253,6 +260,7 @@ class SPOpt(SPBase):
         lib = self._native
         lib.check(self._ctx, lib.objective(self._ctx, self._x.data_ptr(), self._obj_eval.data_ptr(),
                                            self._stream()), "objective")
+        self._bump()
 
     def Ebound(self, verbose=False, extra_sum_terms=None):
         """sum_s p_s * outer_bound_s (+ extra terms), spopt.py:346-391."""

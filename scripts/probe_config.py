@@ -44,7 +44,8 @@ def main():
     print(json.dumps({"config": cfg, "setup_s": t_setup, "ph_main_s": time.time() - t, "tb": tb, "Eobj": E,
                       "conv": conv, "jit": ph._native.jit_info(ph._ctx).decode(),
                       "iterk": getattr(ph, "iterk_stats", None)}))
-    keys = ["wall_s", "not_optimal", "pdhg_iters", "lane_certified", "wg_certified", "wg_ms", "sp_certified",
+    keys = ["wall_s", "not_optimal", "pdhg_iters", "lane_certified", "lane_warm_certified", "lane_ms",
+            "lane_warm_ms", "wg_certified", "wg_ms", "sp_certified",
             "sp_ms", "sp_ipm_its", "sp_warm_rounds", "sp_cold_rounds", "sp_refine", "pdhg_ms", "ipm_ms", "polish_ms"]
     for i, s in enumerate(ph.solve_stats):
         print(i, json.dumps({k: (round(s[k], 3) if isinstance(s.get(k), float) else s.get(k)) for k in keys}))
