@@ -137,6 +137,9 @@ typedef struct phx_solve_stats {
     int32_t sp_cold_rounds;   /* its active-set rounds after the IPM (sum)    */
     int32_t sp_refine;        /* its refinement solves (sum)                  */
     double  sp_ms;            /* sparse solver kernel time                    */
+    int32_t infeasible;       /* scenarios proven infeasible (Farkas
+                                 certificate; status 4): the reference's
+                                 scenario_feasible = False, spopt.py:175-194   */
 } phx_solve_stats;
 
 /* Scenario-tree reduction layout for Compute_Xbar (phbase.py:27-107): for each
@@ -203,7 +206,8 @@ int phx_set_ph_terms(phx_ctx* ctx, const double* W, const double* rho,
  * active-set KKT polish that certifies each scenario's optimum.
  * Outputs (all [.][S]): x_out[n], y_out[m] (row duals), obj_out[S] (objective
  * incl. PH terms, = outer bound), status_out[S] (1 optimal, 2 iteration limit,
- * 3 numerical failure), iters_out[S].  *total_iters_host = iterations run.
+ * 3 numerical failure, 4 infeasible: a Farkas certificate from the interior
+ * point), iters_out[S].  *total_iters_host = iterations run.
  * Synchronises with the host once per check_every iterations.              */
 int phx_solve(phx_ctx* ctx, const phx_solve_opts* opts,
               double* x_out, double* y_out, double* obj_out,

@@ -53,6 +53,7 @@ class SolveStats(ctypes.Structure):
         ("lane_first_certified", c_int32), ("wg_certified", c_int32), ("wg_ms", c_double),
         ("sp_certified", c_int32), ("sp_warm_rounds", c_int32), ("sp_ipm_its", c_int32),
         ("sp_cold_rounds", c_int32), ("sp_refine", c_int32), ("sp_ms", c_double),
+        ("infeasible", c_int32),
     ]
 
 

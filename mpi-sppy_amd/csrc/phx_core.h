@@ -26,7 +26,41 @@
 
 namespace phx {
 
-enum Status : int32_t { RUNNING = 0, OPTIMAL = 1, ITER_LIMIT = 2, NUMERIC_FAIL = 3 };
+// INFEASIBLE: a Farkas certificate proves the subproblem's feasible set empty
+// (the reference's infeasible termination, spopt.py:175-194: scenario_feasible
+// = False); ITER_LIMIT / NUMERIC_FAIL are solve failures, not infeasibility.
+enum Status : int32_t { RUNNING = 0, OPTIMAL = 1, ITER_LIMIT = 2, NUMERIC_FAIL = 3, INFEASIBLE = 4 };
+
+// Farkas test for row weights r: with g = A'r,
+//   min over the column box of g'x  >  max over the row box of r's
+// proves {bl <= A x <= bu, l <= x <= u} empty (every feasible x gives
+// r'A x = r's).  An infeasible problem's interior-point multipliers y
+// (y > 0: lower side, the dual ray of the infeasibility) diverge along such
+// a ray with r = -y, so the failed IPM's -y (normalised) is the candidate.
+// Components below 1e-9 of the largest are taken as zero (an exact ray has
+// zeros there; an infinite bound with a nonzero coefficient voids the test).
+// Accumulate with farkas_col / farkas_row, decide with farkas_margin_ok.
+struct Farkas {
+    double lo = 0.0, hi = 0.0, mag = 0.0;
+    bool ok = true;
+};
+PHX_HD void farkas_col(Farkas& F, double g, double l, double u) {
+    if (fabs(g) <= 1e-9) return;
+    const double b = g > 0.0 ? l : u;
+    if (!isfinite(b)) { F.ok = false; return; }
+    F.lo += g * b;
+    F.mag += fabs(g * b);
+}
+PHX_HD void farkas_row(Farkas& F, double y, double bl, double bu) {
+    if (fabs(y) <= 1e-9) return;
+    const double b = y > 0.0 ? bu : bl;
+    if (!isfinite(b)) { F.ok = false; return; }
+    F.hi += y * b;
+    F.mag += fabs(y * b);
+}
+PHX_HD bool farkas_margin_ok(const Farkas& F) { return F.ok && F.lo - F.hi > 1e-7 * (1.0 + F.mag); }
+
+
 
 // strided scenario vector: element i of scenario s at p[i*si + s*ss]
 struct SVec {
@@ -104,6 +138,27 @@ PHX_HD double aval(const Prob& P, int k, int s) {
 }
 
 PHX_HD double clampd(double v, double lo, double hi) { return fmin(fmax(v, lo), hi); }
+
+// Farkas test of lane s's multipliers y ([m][S], scaled problem).
+PHX_HD bool farkas_lane(const Prob& P, const double* y, int s) {
+    const int S = P.S;
+    double ym = 0.0;
+    for (int i = 0; i < P.m; ++i) ym = fmax(ym, fabs(y[(int64_t)i * S + s]));
+    if (!(ym > 0.0) || !isfinite(ym)) return false;
+    const double iy = -1.0 / ym;        // r = -y / |y|_inf
+    Farkas F;
+    for (int j = 0; j < P.n; ++j) {
+        double g = 0.0;
+        for (int k = P.colptr[j]; k < P.colptr[j + 1]; ++k) {
+            const int kk = P.csc2csr[k];
+            const int v = P.kvar[kk];
+            g += (v < 0 ? P.Ac[kk] : P.Av[(int64_t)v * S + s]) * y[(int64_t)P.rowidx[k] * S + s] * iy;
+        }
+        farkas_col(F, g, P.lb.at(j, s), P.ub.at(j, s));
+    }
+    for (int i = 0; i < P.m; ++i) farkas_row(F, y[(int64_t)i * S + s] * iy, P.bl.at(i, s), P.bu.at(i, s));
+    return farkas_margin_ok(F);
+}
 
 // effective scaled linear cost and diagonal quadratic of column j
 PHX_HD void col_cost(const Prob& P, int j, int s, double& q, double& p) {
@@ -776,6 +831,18 @@ PHX_HD double ipm_lane(const Prob& P, const State& St, const Polish& W, const Ip
         ipm_steps(P, St, I, s, ap, ad);
         ap = fmin(1.0, 0.995 * ap);
         ad = fmin(1.0, 0.995 * ad);
+        // keep the last finite iterate (an infeasible lane's diverging multipliers
+        // are its Farkas ray; a NaN step would erase them)
+        double fin = ap + ad;
+        for (int j = 0; j < n; ++j) {
+            const int64_t o = ix(j, s, S);
+            fin += I.dx[o] + I.dzl[o] + I.dzu[o];
+        }
+        for (int i = 0; i < m; ++i) {
+            const int64_t o = ix(i, s, S);
+            fin += I.ds[o] + I.dwl[o] + I.dwu[o] + I.dy[o];
+        }
+        if (!isfinite(fin)) break;
         for (int j = 0; j < n; ++j) {
             const int64_t o = ix(j, s, S);
             St.xT[o] += ap * I.dx[o];
@@ -809,12 +876,14 @@ PHX_HD void adopt_polished(const Prob& P, const State& St, const Polish& W, int 
     }
 }
 
-// IPM finisher for one lane + polish; returns true when the lane is done.
-PHX_HD bool finish_lane(const Prob& P, const State& St, const Polish& W, const Ipm& I, const Opts& O,
-                        int s) {
+// IPM finisher for one lane + polish; returns the lane's final status
+// (OPTIMAL, or INFEASIBLE with a Farkas certificate from the failed interior
+// point's multipliers), RUNNING when the lane goes on with PDHG.
+PHX_HD int finish_lane(const Prob& P, const State& St, const Polish& W, const Ipm& I, const Opts& O, int s) {
     St.flags[s] |= 1;
     const double e = ipm_lane(P, St, W, I, s, O.ipm_max_it, O.ipm_tol, 1e-10);
     St.err[s] = e;
+    if (!(e < 1e-4) && farkas_lane(P, St.yT, s)) return INFEASIBLE;
     bool done = false;
     if (e < 1e-4 && O.polish) {
         const double tol = fmin(1e-4, fmax(1e-9, 10.0 * e));
@@ -836,7 +905,7 @@ PHX_HD bool finish_lane(const Prob& P, const State& St, const Polish& W, const I
     St.hk[s] = 0;
     St.r0[s] = 1e301;
     St.rprev[s] = 1e301;
-    return done;
+    return done ? OPTIMAL : RUNNING;
 }
 
 // Unscaled outputs + objective (c'x + qN'x_N + 0.5 pN x_N^2 + kN), the value

@@ -611,6 +611,13 @@ PHX_HD double sp_ipm(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds&
         sp_steps(P, G, L, ap, ad);
         ap = fmin(1.0, 0.995 * ap);
         ad = fmin(1.0, 0.995 * ad);
+        // keep the last finite iterate (an infeasible subproblem's diverging
+        // multipliers are its Farkas ray; a NaN step would erase them)
+        double fin[1] = {0.0};
+        for (int j = SP_TID; j < n; j += SP_NT) fin[0] += G.dx[j] + G.dzl[j] + G.dzu[j];
+        for (int i = SP_TID; i < m; i += SP_NT) fin[0] += G.ds[i] + G.dwl[i] + G.dwu[i] + L.tv[i];
+        sp_reduce<1>(fin, L.red, 0);
+        if (!isfinite(fin[0] + ap + ad)) break;
         for (int j = SP_TID; j < n; j += SP_NT) {
             L.xv[j] += ap * G.dx[j];
             G.zl[j] += ad * G.dzl[j];
@@ -792,6 +799,31 @@ PHX_HD int sp_rounds(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds&
     return 0;
 }
 
+// Farkas test (phx_core.h farkas_lane) of the interior point's multipliers in
+// L.yv: a failed IPM on an infeasible subproblem diverges along such a ray.
+PHX_HD bool sp_farkas(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds& L, int s) {
+    double ym[1] = {0.0};
+    for (int i = SP_TID; i < P.m; i += SP_NT) ym[0] = fmax(ym[0], fabs(L.yv[i]));
+    sp_reduce<1>(ym, L.red, 1);
+    if (!(ym[0] > 0.0) || !isfinite(ym[0])) return false;
+    const double iy = -1.0 / ym[0];     // r = -y / |y|_inf (farkas_lane)
+    Farkas F;
+    for (int j = SP_TID; j < P.n; j += SP_NT) {
+        double g = 0.0;
+        for (int k = P.colptr[j]; k < P.colptr[j + 1]; ++k)
+            g += sp_a(P, Y, P.csc2csr[k], s) * L.yv[P.rowidx[k]] * iy;
+        farkas_col(F, g, G.lb[j], G.ub[j]);
+    }
+    for (int i = SP_TID; i < P.m; i += SP_NT) farkas_row(F, L.yv[i] * iy, G.bl[i], G.bu[i]);
+    double v[4] = {F.lo, F.hi, F.mag, F.ok ? 0.0 : 1.0};
+    sp_reduce<3>(v, L.red, 0);
+    double bad[1] = {v[3]};
+    sp_reduce<1>(bad, L.red, 1);
+    Farkas T;
+    T.lo = v[0]; T.hi = v[1]; T.mag = v[2]; T.ok = bad[0] == 0.0;
+    return farkas_margin_ok(T);
+}
+
 // Per-lane counters of one sp solve (for statistics; summed by the host).
 struct SpCount {
     int warm_rounds, ipm_its, cold_rounds, refine;
@@ -800,7 +832,10 @@ struct SpCount {
 // One scenario.  warm: start from the previous solution (St.xT / St.yT); a
 // warm start that does not certify falls back to the interior point.  Returns
 // > 0 (the active-set rounds + interior-point iterations used) when certified;
-// the point is then in L.xv (x, scaled) and L.yv (z = -y, scaled).
+// the point is then in L.xv (x, scaled) and L.yv (z = -y, scaled);
+// SP_INFEASIBLE when the failed interior point's multipliers prove the
+// subproblem infeasible (sp_farkas); 0 otherwise.
+constexpr int SP_INFEASIBLE = -1;
 PHX_HD int sp_solve_one(const Prob& P, const State& St, const SpSym& Y, const SpScr& G, const SpLds& L,
                         const Opts& O, int s, bool warm, int warm_rounds, int cold_rounds, SpCount* cnt) {
     const int S = P.S;
@@ -817,6 +852,7 @@ PHX_HD int sp_solve_one(const Prob& P, const State& St, const SpSym& Y, const Sp
     int its = 0;
     const double e = sp_ipm(P, Y, G, L, s, O.ipm_max_it, O.ipm_tol, 1e-10, &its);
     if (cnt && SP_TID == 0) cnt->ipm_its += its;
+    if (!(e < 1e-4) && sp_farkas(P, Y, G, L, s)) return SP_INFEASIBLE;
     if (e < 1e-4) {
         const double tol = fmin(1e-4, fmax(1e-9, 10.0 * e));
         sp_classify(P, Y, G, L, s, tol);

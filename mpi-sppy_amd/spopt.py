@@ -49,7 +49,7 @@ SOLVER_DEFAULTS = {
     "sp_rounds": 16,
 }
 
-OPTIMAL, ITER_LIMIT, NUMERIC_FAIL = 1, 2, 3
+OPTIMAL, ITER_LIMIT, NUMERIC_FAIL, INFEASIBLE = 1, 2, 3, 4
 
 
 def _overrides(obj, name):
@@ -180,7 +180,7 @@ class SPOpt(SPBase):
         lib = self._native
         stt = _native.SolveStats()
         lib.check(self._ctx, lib.last_solve_stats(self._ctx, ctypes.byref(stt)), "last_solve_stats")
-        n_bad = int(stt.not_optimal)
+        n_bad = int(stt.not_optimal) + int(stt.infeasible)
         t0, gripe = rec.pop("t0"), rec.pop("gripe")
         rec.update({"pdhg_iters": total, "pdhg_ms": stt.pdhg_ms, "launches": stt.pdhg_launches,
                     "lane_iters": stt.lane_iters, "polish_ms": stt.polish_ms, "ipm_ms": stt.ipm_ms,
@@ -192,7 +192,8 @@ class SPOpt(SPBase):
                     "sp_certified": stt.sp_certified, "sp_warm_rounds": stt.sp_warm_rounds,
                     "sp_ipm_its": stt.sp_ipm_its, "sp_cold_rounds": stt.sp_cold_rounds,
                     "sp_refine": stt.sp_refine, "sp_ms": stt.sp_ms,
-                    "wall_s": time.perf_counter() - t0, "not_optimal": n_bad})
+                    "wall_s": time.perf_counter() - t0, "not_optimal": int(stt.not_optimal),
+                    "infeasible": int(stt.infeasible)})
         if n_bad and gripe:
             stc = self._status.cpu().numpy()
             name = self.__class__.__name__
@@ -200,8 +201,8 @@ class SPOpt(SPBase):
                 name = self.spcomm.__class__.__name__
             for k in np.nonzero(stc != OPTIMAL)[0][:10]:
                 print("[%s] Solve failed for scenario %s" % (name, self.local_scenario_names[k]))
-                print("status=", {ITER_LIMIT: "iteration limit", NUMERIC_FAIL: "numerical failure"}.get(
-                    int(stc[k]), int(stc[k])))
+                print("status=", {ITER_LIMIT: "iteration limit", NUMERIC_FAIL: "numerical failure",
+                                  INFEASIBLE: "infeasible"}.get(int(stc[k]), int(stc[k])))
 
     def _sync_solve(self):
         """Finish a deferred solve (phx_solve_finish); returns the number of local

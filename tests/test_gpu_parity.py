@@ -134,6 +134,23 @@ def test_xhat_eval_aircond_gpu(gpu_lib):
     check_aircond_xhat(gpu_lib, None)
 
 
+def test_infeasible_xhat_gpu(gpu_lib):
+    """An xhat over the 500-acre limit on 2,000 scenarios: every subproblem ends
+    INFEASIBLE with a Farkas certificate and infeas_prob() == 1; a feasible xhat
+    afterwards evaluates normally."""
+    from mpisppy_amd.utils.xhat_eval import Xhat_Eval
+    from test_xhat_emu import xhat_options
+    S = 2000
+    ev = Xhat_Eval(xhat_options(), farmer.scenario_names_creator(S), farmer.scenario_creator,
+                   scenario_creator_kwargs={"num_scens": S}, _native_lib=gpu_lib)
+    ev.solve_loop()
+    ev.evaluate({"ROOT": [300.0, 300.0, 300.0]})
+    assert ev.infeas_prob() == pytest.approx(1.0)
+    assert ev.solve_stats[-1]["infeasible"] == S, ev.solve_stats[-1]
+    ev.evaluate({"ROOT": [80.0, 250.0, 170.0]})
+    assert ev.infeas_prob() == 0.0
+
+
 def test_fixed_nonants_large_batch_gpu(gpu_lib):
     """Fixing over 20k scenarios (generic path with per-scenario bounds), sampled
     against the oracle; then unfixing returns to the lane path's solution."""

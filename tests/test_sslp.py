@@ -69,3 +69,34 @@ def check_sslp_ph(lib, device, iters=3):
 
 def test_sslp_ph_emu(emu):
     check_sslp_ph(emu, "cpu", iters=2)
+
+
+def check_sslp_10k(lib, device, S, iters, pick):
+    """BASELINE configs[4] C5a: S stochastic-RHS scenarios (synthetic
+    Bernoulli(0.5) client presence, p = 1/S), `iters` PH iterations: every
+    subproblem of every solve certified; the sampled scenarios' Iter0 optima
+    (unique LP values) and their last-iteration subproblems re-solved by the oracle
+    from the engine's own W / x-bar agree to 1e-8 / 1e-6 (nonants) / 1e-8 (obj)."""
+    names = sslp.scenario_names_creator(S)
+    ph, conv, Eobj, tb = run_engine(sslp.scenario_creator, names, {"num_scens": S}, iters, lib=lib, device=device)
+    assert all(s["not_optimal"] == 0 for s in ph.solve_stats), [s["not_optimal"] for s in ph.solve_stats]
+    o = oph.OraclePH([om.sslp(names[k], num_scens=S) for k in pick], rho=1.0)
+    o.iter0()
+    assert rel(ph._iter0_obj[pick], o.obj) < 1e-8
+    o.W = ph.W_array()[pick].copy()
+    o.xbar = np.tile(ph.xbar_by_node()["ROOT"][0], (len(pick), 1))
+    o.W_on, o.prox_on = 1, 1
+    o.solve_loop()
+    assert rel(ph.nonant_values()[pick], o.xn()) < 1e-6
+    assert rel(ph._host("obj")[pick], o.obj) < 1e-8
+    return ph
+
+
+def test_sslp_synthetic_emu(emu):
+    check_sslp_10k(emu, "cpu", 64, 3, [0, 5, 31, 63])
+
+
+@pytest.mark.gpu
+def test_sslp_10k_gpu(gpu_lib):
+    ph = check_sslp_10k(gpu_lib, None, 10000, 3, [0, 1, 2, 4999, 5000, 9998, 9999])
+    print({k: [s.get(k) for s in ph.solve_stats] for k in ["sp_certified", "wg_certified", "sp_ms", "wg_ms"]})
