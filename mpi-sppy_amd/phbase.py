@@ -378,10 +378,22 @@ class PHBase(SPOpt):
         if getattr(self, "_ar_cb", None) is None:
             bufs = {self._node_stage.data_ptr(): self._node_stage, self._seg_sums.data_ptr(): self._seg_sums}
             comm = self.mpicomm
+            dev = self.device
+            ext = {}
 
             def cb(user, ptr, count, stream):
+                # the collective is enqueued on phx_iterk's own stream (passed in
+                # explicitly), so it orders after the x-bar/segment kernels that
+                # produced the buffer and before the kernels that consume it
                 try:
-                    comm.allreduce_(bufs[ptr][:count])
+                    if dev.type == "cuda" and stream:
+                        s = ext.get(stream)
+                        if s is None:
+                            s = ext[stream] = torch.cuda.ExternalStream(stream, device=dev)
+                        with torch.cuda.stream(s):
+                            comm.allreduce_(bufs[ptr][:count])
+                    else:
+                        comm.allreduce_(bufs[ptr][:count])
                     return 0
                 except Exception as e:   # reported by phx_iterk as a failed all-reduce
                     print("phx_iterk all-reduce callback failed:", repr(e))

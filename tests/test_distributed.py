@@ -33,6 +33,7 @@ def _worker(rank, world, port, out, case):
     from mpisppy_amd.utils import sputils
     emu = _native.Lib(os.path.join(ROOT, "tests", "emu", "libphx_emu.so"), prefix="emu_phx_")
     case, loop = case.split("-")
+    bfs = [5, 2, 2] if case == "aircond3" else [3, 2, 2]
     # native: the device-driven loop (phx_iterk, all-reduce through the
     # callback); host: the Python loop (PHBase methods one by one)
     opts = {"iterk_solver_options": {"native_loop": 1 if loop == "native" else 0}}
@@ -40,8 +41,8 @@ def _worker(rank, world, port, out, case):
         ph, conv, Eobj, tb = run_engine(farmer.scenario_creator, farmer.scenario_names_creator(9),
                                         {"num_scens": 9}, 4, lib=emu, device="cpu", mpicomm=Comm(), options=opts)
     else:
-        bfs = [3, 2, 2]
-        ph, conv, Eobj, tb = run_engine(aircond.scenario_creator, ["scen%d" % i for i in range(12)],
+        S = int(np.prod(bfs))
+        ph, conv, Eobj, tb = run_engine(aircond.scenario_creator, ["scen%d" % i for i in range(S)],
                                         {"branching_factors": bfs, "start_seed": 0}, 3, lib=emu, device="cpu",
                                         mpicomm=Comm(), options=opts,
                                         all_nodenames=sputils.create_nodenames_from_branching_factors(bfs))
@@ -51,29 +52,36 @@ def _worker(rank, world, port, out, case):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("case", ["farmer-native", "farmer-host", "aircond-native", "aircond-host"])
-def test_two_ranks_match_one(emu, case):
+@pytest.mark.parametrize("case", ["farmer-native", "farmer-host", "aircond-native", "aircond-host",
+                                  "aircond3-native"])
+def test_ranks_match_one(emu, case):
+    """2 ranks; aircond3: 3 ranks over 20 scenarios of a 5x2x2 tree (uneven
+    slices 6/7/7 that cut across second-stage nodes) through phx_iterk."""
     from helpers import run_engine
     from mpisppy_amd.examples import aircond, farmer
     from mpisppy_amd.utils import sputils
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_worker, args=(2, _free_port(), out, case), nprocs=2, join=True)
+    world = 3 if case.startswith("aircond3") else 2
+    mp.spawn(_worker, args=(world, _free_port(), out, case), nprocs=world, join=True)
     if case.startswith("farmer"):
         ph, conv, Eobj, tb = run_engine(farmer.scenario_creator, farmer.scenario_names_creator(9), {"num_scens": 9},
                                         4, lib=emu, device="cpu", options={"conv_ranks": 2})
     else:
-        bfs = [3, 2, 2]
-        ph, conv, Eobj, tb = run_engine(aircond.scenario_creator, ["scen%d" % i for i in range(12)],
+        bfs = [5, 2, 2] if case.startswith("aircond3") else [3, 2, 2]
+        S = int(np.prod(bfs))
+        ph, conv, Eobj, tb = run_engine(aircond.scenario_creator, ["scen%d" % i for i in range(S)],
                                         {"branching_factors": bfs, "start_seed": 0}, 3, lib=emu, device="cpu",
-                                        options={"conv_ranks": 2},
+                                        options={"conv_ranks": world},
                                         all_nodenames=sputils.create_nodenames_from_branching_factors(bfs))
-    r0, r1 = out[0], out[1]
-    for r in (r0, r1):
+    rs = [out[r] for r in range(world)]
+    for r in rs:
         assert r[0] == pytest.approx(conv, rel=1e-12)
         assert r[1] == pytest.approx(Eobj, rel=1e-12)
         assert r[2] == pytest.approx(tb, rel=1e-12)
         for k, v in ph.xbar_by_node().items():
             assert np.allclose(r[4][k], v[0], rtol=1e-12, atol=1e-12)
-    W = np.vstack([r0[3], r1[3]])
+    S = len(ph.W_array())
+    assert [len(r[3]) for r in rs] == [int((g + 1) * S / world) - int(g * S / world) for g in range(world)]
+    W = np.vstack([r[3] for r in rs])
     assert np.allclose(W, ph.W_array(), rtol=1e-10, atol=1e-9)
