@@ -32,6 +32,7 @@ struct LaneStructure {
     bool scaled = false;
     std::vector<int32_t> row, col, kvar, col_slot;
     std::vector<int32_t> pair_a, pair_b, pair_pos;
+    std::vector<uint8_t> lnz;   // packed lower triangle: structurally nonzero in L (pairs + fill)
     std::vector<uint8_t> lfin, ufin, fixed, blfin, bufin, eq;
     // scenario-invariant numbers (scaled iff `scaled`), baked into the kernel
     // as literals (c / lb,ub / bl,bu only when they do not vary across
@@ -89,6 +90,15 @@ inline bool build_lane_structure(const HostSetup& hs, int n, int m, int nnz, boo
                 L.pair_pos.push_back(hi * (hi + 1) / 2 + lo);
             }
     L.npairs = (int)L.pair_a.size();
+    // symbolic Cholesky of the normal-matrix pattern (diagonal + pair positions)
+    L.lnz.assign((size_t)m * (m + 1) / 2, 0);
+    for (int i = 0; i < m; ++i) L.lnz[(size_t)i * (i + 1) / 2 + i] = 1;
+    for (int p : L.pair_pos) L.lnz[p] = 1;
+    for (int jj = 0; jj < m; ++jj)
+        for (int i = jj + 1; i < m; ++i)
+            for (int k = 0; k < jj; ++k)
+                if (L.lnz[(size_t)i * (i + 1) / 2 + k] && L.lnz[(size_t)jj * (jj + 1) / 2 + k])
+                    L.lnz[(size_t)i * (i + 1) / 2 + jj] = 1;
     auto uni = [&](const std::vector<double>& a, int S, int len, int j, auto pred) -> int {
         const int v = pred(a[j]) ? 1 : 0;
         for (int s = 1; s < S; ++s)
@@ -143,7 +153,10 @@ inline void emit_dtable(std::ostringstream& o, const char* name, const std::vect
 
 // HIP source of the specialised kernels `phx_lane_ipm` / `phx_lane_polish`
 // (hipRTC input).
-inline std::string lane_kernel_source(const LaneStructure& L, int warm_waves = 1) {
+// with_map: the warm kernels carry the affine-map paths (PHX_LANE_MAP=1);
+// without, that code is compiled out (fewer registers, no spills).
+inline std::string lane_kernel_source(const LaneStructure& L, int warm_waves = 1, bool with_map = false) {
+    const std::string wl = with_map ? "phx_lane::warm_lane<PT, true>" : "phx_lane::warm_lane<PT, false>";
     std::ostringstream o;
     o << "#include \"phx_lane.h\"\n";
     o << "struct PT {\n";
@@ -168,6 +181,7 @@ inline std::string lane_kernel_source(const LaneStructure& L, int warm_waves = 1
     emit_table(o, "int", "pair_a", L.pair_a);
     emit_table(o, "int", "pair_b", L.pair_b);
     emit_table(o, "int", "pair_pos", L.pair_pos);
+    emit_table(o, "bool", "lnz", L.lnz);
     emit_table(o, "bool", "lfin", L.lfin);
     emit_table(o, "bool", "ufin", L.ufin);
     emit_table(o, "bool", "fixed", L.fixed);
@@ -196,18 +210,24 @@ inline std::string lane_kernel_source(const LaneStructure& L, int warm_waves = 1
     // one of its lanes needs a second round.
     o << "extern \"C\" __global__ void __launch_bounds__(64, " << warm_waves
       << ") phx_lane_warm(phx_lane::LaneIO io) {\n"
+         "  phx_lane::lane_stamp(io, 0);\n"
          "  if (phx_lane::gated(io.gate)) return;\n"
          "  if (io.fz.on && !phx_lane::fz_prologue(io)) return;\n"
          "  phx_lane::zero_next_counts(io.counts_next);\n"
+         "  phx_lane::lane_stamp(io, 1);\n"
          "  const int t = blockIdx.x * 64 + threadIdx.x;\n"
          "  bool still = false;\n"
          "  double dl = 0.0;\n"
          "  if (t < io.S) {\n"
          "    if (io.fz.on) dl = phx_lane::fz_update_w<PT>(io, t);\n"
-         "    still = phx_lane::warm_lane<PT>(io, t);\n"
+         "    phx_lane::lane_stamp(io, 2);\n"
+         "    still = " + wl + "(io, t);\n"
          "  }\n"
+         "  phx_lane::lane_stamp(io, 3);\n"
          "  phx_lane::compact_lane(still, t, io.lanes_out, io.count_out);\n"
+         "  phx_lane::lane_stamp(io, 4);\n"
          "  if (io.fz.on) phx_lane::fz_epilogue<PT>(io, t, still, dl);\n"
+         "  phx_lane::lane_stamp(io, 5);\n"
          "}\n";
     // phx_iterk fused mode, after the last enqueued iteration: the decision on
     // its conv (the next warm launch's prologue does it otherwise)
@@ -231,7 +251,7 @@ inline std::string lane_kernel_source(const LaneStructure& L, int warm_waves = 1
          "    const int t = base + threadIdx.x;\n"
          "    bool still = false;\n"
          "    int sc = -1;\n"
-         "    if (t < nl) { sc = lanes[t]; still = phx_lane::warm_lane<PT>(io, sc); }\n"
+         "    if (t < nl) { sc = lanes[t]; still = " + wl + "(io, sc); }\n"
          "    phx_lane::compact_lane(still, sc, io.lanes_out, io.count_out);\n"
          "  }\n"
          "}\n";

@@ -179,7 +179,17 @@ struct LaneIO {
     const int32_t* gate;   // *gate != 0: the launch does nothing (phx_iterk past its stop), or null
     double* map;           // [map_words<PT>()][S] affine solution maps (see map_apply), or null
     FusedW fz;             // phx_iterk fused Update_W (fz.on = 0 otherwise)
+    uint64_t* stamps;      // diagnostics (PHX_LANE_STAMPS=1): [block][8] wall-clock phase stamps, or null
 };
+
+// Phase stamps of phx_lane_warm (lane 0 of each wavefront; 100 MHz wall clock):
+// 0 entry, 1 after the prologue, 2 after Update_W, 3 after the solve,
+// 4 after the compaction, 5 after the epilogue.
+#if defined(__HIPCC__) || defined(__HIPCC_RTC__)
+__device__ __forceinline__ void lane_stamp(const LaneIO& io, int k) {
+    if (io.stamps && threadIdx.x == 0) io.stamps[(uint64_t)blockIdx.x * 8 + k] = wall_clock64();
+}
+#endif
 
 // phx_iterk gate: every kernel of an iteration past the device-side stop exits
 // at once (one scalar load; the counters stay as the last real solve left them)
@@ -205,7 +215,9 @@ struct Data {
             double q = 0.0, p = 0.0;
             if (io.W_on) q = io.W[o];
             if (io.prox_on) {
-                const double r = io.rho[o], xb = io.xbar_node[io.xbar_idx[o]];
+                // fused mode (one tree node, node slot = nonant slot): x-bar of
+                // slot t is stage[t], no index gather
+                const double r = io.rho[o], xb = io.xbar_node[io.fz.on ? t : io.xbar_idx[o]];
                 q -= r * xb;
                 p = r;
                 kn += 0.5 * r * xb * xb;
@@ -282,30 +294,41 @@ struct Data {
     }
 };
 
+// 1/sqrt(d), d > 0: on the GPU the hardware reciprocal square root plus one
+// Newton step (relative error ~1e-14; a correctly rounded sqrt and divide cost
+// ~20 instructions more per pivot, and every solve refines against the
+// factor anyway); on the host (tests/emu) the library functions.
+PHX_LD double rsqrt_pos(double d) {
+#if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC_RTC__)
+    const double y = __builtin_amdgcn_rsq(d);
+    return y * fma(-0.5 * d * y, y, 1.5);
+#else
+    return 1.0 / sqrt(d);
+#endif
+}
+
 // Packed Cholesky (lower, in place).  A pivot that collapses relative to its
 // original diagonal (a dependent row of A D A' near an interior-point
 // optimum) is replaced by a huge value, which zeroes that component of the
 // solve — the classic IPM safeguard.  Returns false only on a non-finite or
 // non-positive original diagonal.
 template <class PT>
-PHX_LD bool cholesky_ipm(double* M, double* idg) {
+PHX_LD bool cholesky_ipm(double* M) {
     bool ok = true;
     PHX_UNROLL for (int jj = 0; jj < PT::m(); ++jj) {
         const double d0 = M[tri(jj, jj)];
         double d = d0;
         PHX_UNROLL for (int k = 0; k < PT::m(); ++k)
-            if (k < jj) d -= M[tri(jj, k)] * M[tri(jj, k)];
+            if (k < jj && PT::lnz(tri(jj, k))) d -= M[tri(jj, k)] * M[tri(jj, k)];
         ok = ok && (d0 > 0.0) && (d0 < 1e300);
         if (!(d > 1e-13 * d0)) d = 1e128;
-        d = sqrt(d);
-        M[tri(jj, jj)] = d;
-        const double inv = 1.0 / d;
-        idg[jj] = inv;
+        const double inv = rsqrt_pos(d);
+        M[tri(jj, jj)] = inv;          // the diagonal keeps 1/L_jj
         PHX_UNROLL for (int i = 0; i < PT::m(); ++i) {
-            if (i > jj) {
+            if (i > jj && PT::lnz(tri(i, jj))) {
                 double v = M[tri(i, jj)];
                 PHX_UNROLL for (int k = 0; k < PT::m(); ++k)
-                    if (k < jj) v -= M[tri(i, k)] * M[tri(jj, k)];
+                    if (k < jj && PT::lnz(tri(i, k)) && PT::lnz(tri(jj, k))) v -= M[tri(i, k)] * M[tri(jj, k)];
                 M[tri(i, jj)] = v * inv;
             }
         }
@@ -314,24 +337,26 @@ PHX_LD bool cholesky_ipm(double* M, double* idg) {
 }
 
 // Plain packed Cholesky; false if not (numerically) positive definite.
-// idg[i] receives 1/L_ii for the multiplication-only solve.
+// Every packed routine touches only the entries of L's symbolic pattern
+// PT::lnz (the pair positions of A A' plus the Cholesky fill, phx_jit.h):
+// entries outside it stay exact zeros, so skipping them changes no bit.
+// The diagonal receives 1/L_ii (the solve multiplies).
 template <class PT>
-PHX_LD bool cholesky(double* M, double* idg) {
+PHX_LD bool cholesky(double* M) {
     bool ok = true;
     PHX_UNROLL for (int jj = 0; jj < PT::m(); ++jj) {
         double d = M[tri(jj, jj)];
         PHX_UNROLL for (int k = 0; k < PT::m(); ++k)
-            if (k < jj) d -= M[tri(jj, k)] * M[tri(jj, k)];
+            if (k < jj && PT::lnz(tri(jj, k))) d -= M[tri(jj, k)] * M[tri(jj, k)];
         ok = ok && (d > 0.0);
-        d = sqrt(fmax(d, 1e-300));
-        M[tri(jj, jj)] = d;
-        const double inv = 1.0 / d;
-        idg[jj] = inv;
+        d = fmax(d, 1e-300);
+        const double inv = rsqrt_pos(d);
+        M[tri(jj, jj)] = inv;          // the diagonal keeps 1/L_jj
         PHX_UNROLL for (int i = 0; i < PT::m(); ++i) {
-            if (i > jj) {
+            if (i > jj && PT::lnz(tri(i, jj))) {
                 double v = M[tri(i, jj)];
                 PHX_UNROLL for (int k = 0; k < PT::m(); ++k)
-                    if (k < jj) v -= M[tri(i, k)] * M[tri(jj, k)];
+                    if (k < jj && PT::lnz(tri(i, k)) && PT::lnz(tri(jj, k))) v -= M[tri(i, k)] * M[tri(jj, k)];
                 M[tri(i, jj)] = v * inv;
             }
         }
@@ -339,21 +364,21 @@ PHX_LD bool cholesky(double* M, double* idg) {
     return ok;
 }
 
-// solve (L L') t = t with the reciprocal diagonal idg
+// solve (L L') t = t (L's diagonal stored as its reciprocal)
 template <class PT>
-PHX_LD void chol_solve_inv(const double* M, const double* idg, double* t) {
+PHX_LD void chol_solve_inv(const double* M, double* t) {
     PHX_UNROLL for (int i = 0; i < PT::m(); ++i) {
         double v = t[i];
         PHX_UNROLL for (int k = 0; k < PT::m(); ++k)
-            if (k < i) v -= M[tri(i, k)] * t[k];
-        t[i] = v * idg[i];
+            if (k < i && PT::lnz(tri(i, k))) v -= M[tri(i, k)] * t[k];
+        t[i] = v * M[tri(i, i)];
     }
     PHX_UNROLL for (int ii = 0; ii < PT::m(); ++ii) {
         const int i = PT::m() - 1 - ii;
         double v = t[i];
         PHX_UNROLL for (int k = 0; k < PT::m(); ++k)
-            if (k > i) v -= M[tri(k, i)] * t[k];
-        t[i] = v * idg[i];
+            if (k > i && PT::lnz(tri(k, i))) v -= M[tri(k, i)] * t[k];
+        t[i] = v * M[tri(i, i)];
     }
 }
 
@@ -446,7 +471,7 @@ PHX_LD double ipm_core(const Data<PT>& D, int max_it, double tol, double* x, dou
         }
         mu *= inv_ncomp;
         // normal matrix
-        double Dx[NN], isig[MM], M[TT], idg[MM];
+        double Dx[NN], isig[MM], M[TT];
         PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
             double h = D.p(j) + reg;
             if (has_lo<PT>(j)) h += zl[j] * rl[j];
@@ -466,7 +491,7 @@ PHX_LD double ipm_core(const Data<PT>& D, int max_it, double tol, double* x, dou
             if (!row_free<PT>(PT::row(ka)) && !row_free<PT>(PT::row(kb)))
                 M[PT::pair_pos(t)] += D.A(ka) * Dx[PT::col(ka)] * D.A(kb);
         }
-        if (!cholesky_ipm<PT>(M, idg)) { PHX_LANE_FAIL(20, it); break; }
+        if (!cholesky_ipm<PT>(M)) { PHX_LANE_FAIL(20, it); break; }
         // predictor (pass 0, smu = 0) then corrector (pass 1)
         double smu = 0.0, ap = 1.0, ad = 1.0;
         double dx[NN], ds[MM], dy[MM], dxa[NN], dsa[MM];
@@ -507,7 +532,7 @@ PHX_LD double ipm_core(const Data<PT>& D, int max_it, double tol, double* x, dou
                     else dy[i] = -(ax[i] - s[i]) + rhos * isig[i] - ahr[i];
                 }
             }
-            chol_solve_inv<PT>(M, idg, dy);
+            chol_solve_inv<PT>(M, dy);
             {
                 double atdy[NN];
                 D.matvec_t(dy, atdy);
@@ -727,7 +752,7 @@ PHX_LD void classify(const Data<PT>& D, const double* xv, const double* yv, doub
 // columns.
 template <class PT>
 struct KFactor {
-    double M[PT::NMAX_M * (PT::NMAX_M + 1) / 2], idg[PT::NMAX_M];
+    double M[PT::NMAX_M * (PT::NMAX_M + 1) / 2];
     double ipn[PT::NMAX_S];
     PHX_LD double Hinv(int j) const { return PT::col_slot(j) >= 0 ? ipn[PT::col_slot(j)] : 1.0 / KKT_REG; }
 };
@@ -747,7 +772,7 @@ PHX_LD bool kkt_factor(const Data<PT>& D, const ASet<PT>& a, KFactor<PT>& K) {
         if (a.R(PT::row(ka)) && a.R(PT::row(kb)) && a.F(PT::col(ka)))
             K.M[PT::pair_pos(t)] += D.A(ka) * K.Hinv(PT::col(ka)) * D.A(kb);
     }
-    if (!cholesky<PT>(K.M, K.idg)) { PHX_LANE_FAIL(10, -1); return false; }
+    if (!cholesky<PT>(K.M)) { PHX_LANE_FAIL(10, -1); return false; }
     return true;
 }
 
@@ -763,44 +788,54 @@ PHX_LD void kkt_refine(const Data<PT>& D, const ASet<PT>& a, const KFactor<PT>& 
     PHX_UNROLL for (int j = 0; j < PT::n(); ++j)
         if (!a.F(j)) xp[j] = R.xb(j);
     PHX_UNROLL for (int i = 0; i < PT::m(); ++i) if (!a.R(i)) z[i] = 0.0;
+    // the free columns as a multiplier, once: hf = H^-1 on free columns and 0
+    // elsewhere; the column loops then run without selects (non-free
+    // components get exact zero corrections, so xp keeps its bound values bit
+    // for bit)
+    double hf[NN];
+    PHX_UNROLL for (int j = 0; j < PT::n(); ++j) hf[j] = a.F(j) ? K.Hinv(j) : 0.0;
     PHX_REFINE_LOOP for (int it = 0; it < KKT_REFINE; ++it) {
-        double r1[NN], t[MM];
+        double g[NN], t[MM];
         {
             double atz[NN];
             D.matvec_t(z, atz);
-            PHX_UNROLL for (int j = 0; j < PT::n(); ++j)
-                r1[j] = a.F(j) ? -R.q(j) - D.p(j) * xp[j] - atz[j] : 0.0;
+            PHX_UNROLL for (int j = 0; j < PT::n(); ++j) g[j] = -R.q(j) - D.p(j) * xp[j] - atz[j];
         }
         {
             double axp[MM], hr[NN], ahr[MM];
             D.matvec(xp, axp);
-            PHX_UNROLL for (int j = 0; j < PT::n(); ++j) hr[j] = r1[j] * K.Hinv(j);   // r1 = 0 off F
+            PHX_UNROLL for (int j = 0; j < PT::n(); ++j) hr[j] = g[j] * hf[j];
             D.matvec(hr, ahr);
-            PHX_UNROLL for (int i = 0; i < PT::m(); ++i)
-                t[i] = a.R(i) ? ahr[i] - (R.b(i) - axp[i]) : 0.0;
+            // (a select: the inactive side of a row may be infinite)
+            PHX_UNROLL for (int i = 0; i < PT::m(); ++i) t[i] = a.R(i) ? ahr[i] - (R.b(i) - axp[i]) : 0.0;
         }
-        chol_solve_inv<PT>(K.M, K.idg, t);
+        chol_solve_inv<PT>(K.M, t);   // inactive rows: identity, t stays 0
         double atdz[NN];
         D.matvec_t(t, atdz);
-        double dmax = 0.0, xmax = 0.0;
-        PHX_UNROLL for (int j = 0; j < PT::n(); ++j)
-            if (a.F(j)) {
-                const double d = (r1[j] - atdz[j]) * K.Hinv(j);
-                xp[j] += d;
-                dmax = fmax(dmax, fabs(d));
-                xmax = fmax(xmax, fabs(xp[j]));
-            }
-        PHX_UNROLL for (int i = 0; i < PT::m(); ++i)
-            if (a.R(i)) {
-                z[i] += t[i];
-                dmax = fmax(dmax, fabs(t[i]));
-                xmax = fmax(xmax, fabs(z[i]));
-            }
+        double d2 = 0.0, x2 = 0.0;
+        PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
+            const double d = (g[j] - atdz[j]) * hf[j];
+            xp[j] += d;
+            d2 += d * d;
+            x2 += xp[j] * xp[j];
+        }
+        PHX_UNROLL for (int i = 0; i < PT::m(); ++i) {
+            z[i] += t[i];
+            d2 += t[i] * t[i];
+            x2 += z[i] * z[i];
+        }
         PHX_LANE_STAT(1);
-        // stop once the correction vanishes (1e-10 relative): the certificate's
-        // tolerance is relative to the problem's scale, so it cannot stand in
-        // for this (a looser stop, 1e-5, passed certificates at 1e-7 accuracy)
-        if (dmax <= KKT_STOP * (1.0 + xmax)) break;
+        // stop once the correction vanishes (1e-10 relative, in squared 2-norms:
+        // |d|^2 <= stop^2 (1 + |x|^2)): the certificate's tolerance is
+        // relative to the problem's scale, so it cannot stand in for this (a
+        // looser stop, 1e-5, passed certificates at 1e-7 accuracy).  (Skipping
+        // the confirming step on a predicted geometric contraction was tried:
+        // it leaves errors at the stop's scale, 1e-9 in aircond's W; so was
+        // stopping when a step does not contract: on degenerate LPs the
+        // refinement is not monotone, and the cut rounds moved the active set
+        // to another optimal vertex.)
+        const double tol2 = KKT_STOP * KKT_STOP * (1.0 + x2);
+        if (d2 <= tol2) break;
     }
 }
 
@@ -1006,7 +1041,7 @@ PHX_LD void write_certified(const LaneIO& io, const Data<PT>& D, int sc, const A
 // ---------------------------------------------------------------------------
 // Kernel bodies.  Both return true if the lane still needs the generic path.
 // ---------------------------------------------------------------------------
-template <class PT>
+template <class PT, bool MAP = true>
 PHX_LD bool warm_lane(const LaneIO& io, int sc) {
     constexpr int NN = PT::NMAX_N, MM = PT::NMAX_M;
     const Data<PT> D(io, sc);
@@ -1015,7 +1050,7 @@ PHX_LD bool warm_lane(const LaneIO& io, int sc) {
     double xp[NN], z[MM];
     PHX_UNROLL for (int j = 0; j < PT::n(); ++j) xp[j] = 0.0;
     PHX_UNROLL for (int i = 0; i < PT::m(); ++i) z[i] = 0.0;
-    if (io.map && (io.flags[sc] & FLAG_MAP) && map_apply<PT>(D, io, sc, xp, z)) {
+    if (MAP && io.map && (io.flags[sc] & FLAG_MAP) && map_apply<PT>(D, io, sc, xp, z)) {
         PHX_LANE_STAT(2);
         // the same active set, so the same certificate as a KKT solve's
         const int c = certify_update<PT>(D, a, xp, z, io.kkt_tol);
@@ -1026,7 +1061,7 @@ PHX_LD bool warm_lane(const LaneIO& io, int sc) {
         // the active set moved: rounds from the updated set, warm from (xp, z)
     }
     if (as_rounds<PT>(D, a, io, io.warm_rounds, xp, z)) {
-        const bool mok = io.map && map_compute<PT>(D, a, io, sc);
+        const bool mok = MAP && io.map && map_compute<PT>(D, a, io, sc);
         write_certified<PT>(io, D, sc, a, xp, z, 0, mok);
         return false;
     }

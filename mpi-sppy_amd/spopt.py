@@ -422,10 +422,30 @@ class SPOpt(SPBase):
         self._set_nonant_x(self.nonant_cache)
 
     def _save_original_nonants(self):
-        """original_nonants / original_fixedness (spopt.py:690-710)."""
+        """original_nonants / original_fixedness (spopt.py:690-710).  The values are
+        kept as a device copy (one gather, no host round trip inside Iter0);
+        ``original_nonants`` reads them back on first use."""
         fixed, _ = self._fix_arrays()
-        self.original_nonants = np.ascontiguousarray(self._nonant_x())
+        self._settle()
+        S = self._S
+        cols = torch.as_tensor(self.batch.nonant.slot_col.astype(np.int64), device=self.device)
+        self._orig_nonants_dev = self._x.view(-1, S)[cols].clone()
+        self._orig_nonants_host = None
         self.original_fixedness = fixed.copy()
+
+    @property
+    def original_nonants(self):
+        if getattr(self, "_orig_nonants_host", None) is None:
+            dev = getattr(self, "_orig_nonants_dev", None)
+            if dev is None:
+                raise AttributeError("original_nonants: _save_original_nonants has not run")
+            self._orig_nonants_host = np.ascontiguousarray(dev.cpu().numpy().T)
+        return self._orig_nonants_host
+
+    @original_nonants.setter
+    def original_nonants(self, vals):
+        self._orig_nonants_host = np.ascontiguousarray(np.asarray(vals, dtype=np.float64))
+        self._orig_nonants_dev = None
 
     def _restore_original_nonants(self):
         """spopt.py:713-741."""

@@ -2,27 +2,51 @@
 with the gfx950 FETCH_SIZE correction (MI355X_MICROARCH.md, HBM section:
 FETCH_SIZE reports half the bytes of a coalesced streaming read -> x2).
 
-    python scripts/pmc_summary.py KERNEL dir1 [dir2 ...] > profiles/xxx.json
+    python scripts/pmc_summary.py KERNEL [--last N] dir1 [dir2 ...] > profiles/xxx.json
+
+--last N keeps the last N launches of KERNEL in each pass (by dispatch id): the
+timed window of a bench run that ends with its timed iterations (--no-conv).
 """
 import collections
 import csv
 import glob
 import json
 import os
+import sqlite3
 import sys
 
 
-def main(kernel, dirs):
-    out = {"kernel": kernel, "counters": {}, "launches": {}}
+def main(kernel, dirs, last=None):
+    out = {"kernel": kernel, "counters": {}, "launches": {}, "window": "last %d launches" % last if last else "all"}
     for d in dirs:
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
-            agg = collections.defaultdict(list)
+            agg = collections.defaultdict(lambda: collections.defaultdict(float))
             for r in csv.DictReader(open(f)):
                 if r["Kernel_Name"].split("(")[0] == kernel:
-                    agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
-            for k, v in agg.items():
-                out["counters"][k] = sum(v) / len(v)
-                out["launches"][k] = len(v)
+                    agg[r["Counter_Name"]][int(r["Dispatch_Id"])] += float(r["Counter_Value"])
+            add(agg, out, last)
+        for f in glob.glob(os.path.join(d, "**", "*results.db"), recursive=True):
+            agg = collections.defaultdict(lambda: collections.defaultdict(float))
+            con = sqlite3.connect(f)
+            for name, disp, ctr, val in con.execute(
+                    "select kernel_name, dispatch_id, counter_name, value from counters_collection"):
+                if name.split("(")[0] == kernel:
+                    agg[ctr][int(disp)] += float(val)
+            add(agg, out, last)
+    finish(out)
+
+
+def add(agg, out, last):
+    """per-dispatch sums -> mean over the (last) launches"""
+    for k, per in agg.items():
+        v = [per[i] for i in sorted(per)]
+        if last:
+            v = v[-last:]
+        out["counters"][k] = sum(v) / len(v)
+        out["launches"][k] = len(v)
+
+
+def finish(out):
     c = out["counters"]
     if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
         fetch = 2.0 * c["FETCH_SIZE"] * 1024.0      # KiB -> bytes, x2 gfx950 correction
@@ -32,4 +56,10 @@ def main(kernel, dirs):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2:])
+    a = sys.argv[1:]
+    last = None
+    if "--last" in a:
+        i = a.index("--last")
+        last = int(a[i + 1])
+        del a[i:i + 2]
+    main(a[0], a[1:], last)
