@@ -75,6 +75,8 @@ namespace phx_lane {
 
 PHX_LD int tri(int i, int k) { return i * (i + 1) / 2 + k; }   // i >= k
 PHX_LD double clampd(double v, double lo, double hi) { return fmin(fmax(v, lo), hi); }
+template <bool B, class T, class E> struct Cond { typedef T type; };
+template <class T, class E> struct Cond<false, T, E> { typedef E type; };
 
 // active-set words: 2 bits per column (0 free, 1 at lower, 2 at upper) then
 // 2 bits per row (0 inactive, 1 lower side active, 2 upper side active)
@@ -497,7 +499,7 @@ PHX_LD double ipm_core(const Data<PT>& D, int max_it, double tol, double* x, dou
         double dx[NN], ds[MM], dy[MM], dxa[NN], dsa[MM];
         PHX_UNROLL for (int j = 0; j < PT::n(); ++j) dxa[j] = 0.0;
         PHX_UNROLL for (int i = 0; i < PT::m(); ++i) dsa[i] = 0.0;
-        for (int pass = 0; pass < 2; ++pass) {
+        PHX_NOUNROLL for (int pass = 0; pass < 2; ++pass) {
             {
                 double ax[MM], aty[NN];
                 D.matvec(x, ax);
@@ -645,8 +647,6 @@ PHX_LD double ipm_core(const Data<PT>& D, int max_it, double tol, double* x, dou
 // ---------------------------------------------------------------------------
 // Kept as per-lane bit masks in vector registers (per-lane bool arrays would
 // become 64-bit exec-style lane masks in scalar registers and spill).
-template <bool B, class T, class E> struct Cond { typedef T type; };
-template <class T, class E> struct Cond<false, T, E> { typedef E type; };
 
 template <class PT>
 struct ASet {
@@ -1010,7 +1010,7 @@ PHX_LD bool as_rounds(const Data<PT>& D, ASet<PT>& a, const LaneIO& io, int roun
         if (!kkt_solve<PT>(D, a, xp, z)) return false;
         const int c = certify_update<PT>(D, a, xp, z, io.kkt_tol);
         if (c == 0) return true;
-        if (c == 2) return false;
+        if (c == 2) { PHX_LANE_STAT(3); return false; }
     }
     return false;
 }
