@@ -20,7 +20,7 @@ import torch.distributed as dist
 class Comm:
     def __init__(self, group=None):
         self.group = group
-        if dist.is_available() and dist.is_initialized():
+        if group is not None or (dist.is_available() and dist.is_initialized()):
             self.rank = dist.get_rank(group)
             self.size = dist.get_world_size(group)
             self.backend = dist.get_backend(group)
@@ -68,8 +68,39 @@ class Comm:
         if self.size == 1:
             return obj
         lst = [obj]
-        dist.broadcast_object_list(lst, src=root, group=self.group)
+        # broadcast_object_list takes a GLOBAL source rank
+        src = dist.get_global_rank(self.group, root) if self.group is not None else root
+        dist.broadcast_object_list(lst, src=src, group=self.group)
         return lst[0]
+
+    def allreduce_np(self, arr, op="sum"):
+        """Allreduce of a small host array (write ids, flags): on a GPU tensor
+        for RCCL groups, on the host for gloo.  Returns a new numpy array."""
+        import numpy as np
+        a = np.asarray(arr)
+        if self.size == 1:
+            return a.copy()
+        t = torch.as_tensor(a.copy())
+        if self.backend == "nccl":
+            t = t.to("cuda")
+        rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
+        dist.all_reduce(t, op=rop, group=self.group)
+        return t.cpu().numpy()
+
+    def Split(self, color, key):
+        """mpi4py's ``Comm.Split``: ranks with the same color form a new
+        communicator, ordered by key.  Every rank of this communicator must
+        call it (torch.distributed creates each group collectively)."""
+        if self.size == 1:
+            return Comm(self.group)
+        entries = self.allgather_object((int(color), int(key), dist.get_rank()))
+        mine = None
+        for c in sorted({e[0] for e in entries}):
+            members = [g for (cc, k, g) in sorted((e for e in entries if e[0] == c), key=lambda e: (e[1], e[2]))]
+            grp = dist.new_group(ranks=members)
+            if c == int(color):
+                mine = grp
+        return Comm(mine)
 
 
 def world():

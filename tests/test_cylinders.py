@@ -1,0 +1,199 @@
+"""Hub and spokes as separate processes: a PHHub
+running PH and a LagrangianOuterBound spoke, started by WheelSpinner over
+torch.distributed (gloo) with the node-local shared-memory windows, on CPU
+through the ABI emulation.
+
+Checked against the reference's semantics (hub.py:370-598, spoke.py:60-208,
+lagrangian_bounder.py:9-95, spin_the_wheel.py:34-159):
+* wire format: the spoke reads `[W (S*N) | outer, inner, write_id]`, every
+  bound it reports arrives with a write id, the kill signal is write id -1;
+* every Lagrangian bound the spoke reported equals the oracle's Lagrangian bound
+  (W on, prox off, exact LP/QP solves) for the hub's W of that write id;
+* the hub's best outer bound is the best of those and the trivial bound, and
+  lies below the EF optimum;
+* 2 ranks per cylinder (world 4): scenarios sharded over the cylinder, write
+  ids agreed across the cylinder's ranks, the same bounds as with 1 rank.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+S = 12
+ITERS = 6
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import mpisppy_amd  # noqa: F401
+    from mpisppy_amd import _native
+    from mpisppy_amd.comm import Comm
+    from mpisppy_amd.cylinders import LagrangianOuterBound, PHHub
+    from mpisppy_amd.examples import farmer
+    from mpisppy_amd.opt.ph import PH
+    from mpisppy_amd.phbase import PHBase
+    from mpisppy_amd.spin_the_wheel import WheelSpinner
+    from helpers import ph_options
+    emu = _native.Lib(os.path.join(ROOT, "tests", "emu", "libphx_emu.so"), prefix="emu_phx_")
+    names = farmer.scenario_names_creator(S)
+
+    sent = []       # the hub's W per write id
+    got = []        # the spoke's (write id, bound) per Lagrangian pass
+
+    class RecordingHub(PHHub):
+        def send_ws(self):
+            super().send_ws()
+            sent.append((int(self.w_send_buffer[-1]), self.w_send_buffer[:-3].copy()))
+
+    class RecordingSpoke(LagrangianOuterBound):
+        def lagrangian(self):
+            b = super().lagrangian()
+            got.append((int(self.get_serial_number()), b, self.localWs.copy()))
+            return b
+
+    okw = dict(options=ph_options(ITERS), all_scenario_names=names, scenario_creator=farmer.scenario_creator,
+               scenario_creator_kwargs={"num_scens": S}, _native_lib=emu, _device="cpu")
+    hub_dict = {"hub_class": RecordingHub, "hub_kwargs": {"options": {"display_progress": False}},
+                "opt_class": PH, "opt_kwargs": dict(okw)}
+    spoke_dict = {"spoke_class": RecordingSpoke, "opt_class": PHBase, "opt_kwargs": dict(okw)}
+    wheel = WheelSpinner(hub_dict, [spoke_dict])
+    wheel.spin(comm_world=Comm())
+    sp = wheel.spcomm
+    rec = {"strata_rank": wheel.strata_rank, "cylinder_rank": wheel.cylinder_rank,
+           "local_names": list(sp.opt.local_scenario_names)}
+    if wheel.strata_rank == 0:
+        rec.update(best_outer=wheel.BestOuterBound, best_inner=wheel.BestInnerBound,
+                   trivial=sp.opt.trivial_bound, sent=sent, write_ids=sp.local_write_ids.tolist(),
+                   remote_ids=sp.remote_write_ids.tolist(), on_hub=wheel.on_hub(),
+                   W=sp.opt.W_array())
+    else:
+        rec.update(got=got, final=sp.final_bound, remote_id=sp.remote_write_id,
+                   local_id=sp.local_write_id, on_hub=wheel.on_hub())
+    out[rank] = rec
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _run(world):
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    return [out[r] for r in range(world)]
+
+
+def _oracle_lagrangian(W_flat):
+    from oracle import models as om, ph as oph
+    names = ["scen%d" % i for i in range(S)]
+    o = oph.OraclePH([om.farmer(n, num_scens=S) for n in names], rho=1.0)
+    o.W = np.asarray(W_flat, dtype=np.float64).reshape(S, -1).copy()
+    o.W_on, o.prox_on = 1, 0
+    o.solve_loop()
+    return o.Ebound()
+
+
+def _check(res, ncyl):
+    from oracle import models as om, ph as oph
+    hubs = [r for r in res if r["strata_rank"] == 0]
+    spokes = [r for r in res if r["strata_rank"] == 1]
+    assert len(hubs) == ncyl and len(spokes) == ncyl
+    assert all(h["on_hub"] for h in hubs) and not any(s["on_hub"] for s in spokes)
+    # every cylinder covers all scenarios once (contiguous slices)
+    for grp in (hubs, spokes):
+        allnames = sorted(n for r in grp for n in r["local_names"])
+        assert allnames == sorted("scen%d" % i for i in range(S))
+    h0 = hubs[0]
+    # sync after Iter0 and after every iteration: ITERS + 1 W sends, ids 1..ITERS+1
+    ids = [i for i, _ in h0["sent"]]
+    assert ids == list(range(1, ITERS + 2))
+    assert h0["write_ids"] == [ITERS + 1]
+    # full W vectors by write id (cylinder ranks hold slices: concatenate by rank)
+    hub_ranks = sorted(hubs, key=lambda r: r["cylinder_rank"])
+    W_by_id = {i: np.concatenate([dict(r["sent"])[i] for r in hub_ranks]) for i in ids}
+    W_by_id[0] = np.zeros(S * 3)
+    # the hub's final W is the last one sent (after the last iteration's solve)
+    assert np.array_equal(np.concatenate([r["W"].ravel() for r in hub_ranks]), W_by_id[ITERS + 1])
+    sp_ranks = sorted(spokes, key=lambda r: r["cylinder_rank"])
+    g0 = sp_ranks[0]["got"]
+    assert len(g0) >= 2
+    # all spoke ranks ran the same passes with the same serial numbers and bounds
+    for r in sp_ranks[1:]:
+        assert [(i, b) for i, b, _ in r["got"]] == [(i, b) for i, b, _ in g0]
+    # kill signal seen; the final pass ran on the kill buffer's zeros (reference quirk)
+    assert all(r["remote_id"] == -1 for r in sp_ranks)
+    bounds = []
+    for k, (wid, b, _) in enumerate(g0):
+        Wloc = np.concatenate([r["got"][k][2] for r in sp_ranks])
+        if k == len(g0) - 1:               # finalize(): the buffer holds the kill signal's zeros
+            assert not Wloc.any()
+            continue
+        assert np.array_equal(Wloc, W_by_id[wid]), wid
+        ob = _oracle_lagrangian(W_by_id[wid])
+        assert b == pytest.approx(ob, rel=1e-9, abs=1e-7), (wid, b, ob)
+        bounds.append(b)
+    # the spoke's first bound is the trivial bound (W = 0, serial number 0)
+    assert g0[0][0] == 0 and g0[0][1] == pytest.approx(h0["trivial"], rel=1e-12)
+    # the hub holds the best (largest: minimisation) bound it received, never worse than trivial
+    ef, _, _ = oph.solve_ef([om.farmer("scen%d" % i, num_scens=S) for i in range(S)])
+    assert h0["best_outer"] >= h0["trivial"] - 1e-9
+    assert h0["best_outer"] <= ef + 1e-6 * abs(ef)
+    # (the hub sees the values it happened to read: not every bound the spoke wrote)
+    assert h0["best_outer"] in bounds + [h0["trivial"]]
+    assert h0["best_outer"] <= max(bounds + [h0["trivial"]])
+    assert h0["best_inner"] == float("inf")
+    return [b for b in bounds]
+
+
+def test_wheel_lagrangian_1x(emu):
+    _check(_run(2), 1)
+
+
+def test_wheel_lagrangian_2x(emu):
+    """Two ranks per cylinder: sharded scenarios, write-id agreement."""
+    _check(_run(4), 2)
+
+
+def test_window_seqlock_roundtrip():
+    """The window's epoch protocol within one process: put / get round trip,
+    write id slot, kill signal, and a torn epoch (odd sequence) is not read."""
+    from mpisppy_amd.cylinders.spwindow import SPWindow
+    a = SPWindow("t%d" % os.getpid(), 0, 0, [5, 3])
+    b = SPWindow("t%d" % os.getpid(), 0, 1, [5, 3])
+    try:
+        v = np.arange(6, dtype=np.float64)
+        v[-1] = 7
+        a.put(v)
+        out = np.zeros(6)
+        b.get(0, out)
+        assert np.array_equal(out, v)
+        k = np.zeros(4)
+        k[-1] = -1
+        b.put(k)
+        o2 = np.zeros(4)
+        a.get(1, o2)
+        assert o2[-1] == -1
+        seq = SPWindow._seq(a._own)
+        seq[0] += 1                       # a writer in the middle of an epoch
+        with pytest.raises(RuntimeError):
+            b.get(0, out, timeout=0.05)
+        seq[0] += 1
+        b.get(0, out)
+    finally:
+        out = o2 = None
+        a.free()
+        b.free()
