@@ -5,3 +5,4 @@ from .spoke import (ConvergerSpokeType, Spoke, InnerBoundSpoke, OuterBoundSpoke,
                     InnerBoundNonantSpoke, OuterBoundNonantSpoke)
 from .hub import Hub, PHHub  # noqa: F401
 from .lagrangian_bounder import LagrangianOuterBound  # noqa: F401
+from .xhatxbar_bounder import XhatXbarInnerBound  # noqa: F401

@@ -12,7 +12,10 @@ lagrangian_bounder.py:9-95, spin_the_wheel.py:34-159):
 * the hub's best outer bound is the best of those and the trivial bound, and
   lies below the EF optimum;
 * 2 ranks per cylinder (world 4): scenarios sharded over the cylinder, write
-  ids agreed across the cylinder's ranks, the same bounds as with 1 rank.
+  ids agreed across the cylinder's ranks, the same bounds as with 1 rank;
+* three cylinders (hub + Lagrangian + x-bar inner bound, xhatxbar_bounder.py:31-114):
+  the hub terminates on rel_gap (hub.py:125-161), each inner bound is the
+  oracle's x-bar evaluation of the nonants it came from.
 """
 import os
 import socket
@@ -166,6 +169,81 @@ def test_wheel_lagrangian_1x(emu):
 def test_wheel_lagrangian_2x(emu):
     """Two ranks per cylinder: sharded scenarios, write-id agreement."""
     _check(_run(4), 2)
+
+
+def _worker3(rank, world, port, out):
+    """hub + Lagrangian outer bound + x-bar inner bound, gap termination."""
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import mpisppy_amd  # noqa: F401
+    from mpisppy_amd import _native
+    from mpisppy_amd.comm import Comm
+    from mpisppy_amd.cylinders import LagrangianOuterBound, PHHub, XhatXbarInnerBound
+    from mpisppy_amd.examples import farmer
+    from mpisppy_amd.opt.ph import PH
+    from mpisppy_amd.phbase import PHBase
+    from mpisppy_amd.spin_the_wheel import WheelSpinner
+    from mpisppy_amd.utils.xhat_eval import Xhat_Eval
+    from helpers import ph_options
+    emu = _native.Lib(os.path.join(ROOT, "tests", "emu", "libphx_emu.so"), prefix="emu_phx_")
+    names = farmer.scenario_names_creator(S)
+    tried = []
+
+    class RecordingXhat(XhatXbarInnerBound):
+        def update_if_improving(self, b):
+            tried.append((self.localnonants.copy(), b))
+            return super().update_if_improving(b)
+
+    okw = dict(options=ph_options(200), all_scenario_names=names, scenario_creator=farmer.scenario_creator,
+               scenario_creator_kwargs={"num_scens": S}, _native_lib=emu, _device="cpu")
+    xopts = dict(ph_options(200))
+    xopts["xhat_xbar_options"] = {"xhat_solver_options": {}}
+    hub_dict = {"hub_class": PHHub, "hub_kwargs": {"options": {"rel_gap": 0.01, "display_progress": False}},
+                "opt_class": PH, "opt_kwargs": dict(okw)}
+    spokes = [{"spoke_class": LagrangianOuterBound, "opt_class": PHBase, "opt_kwargs": dict(okw)},
+              {"spoke_class": RecordingXhat, "opt_class": Xhat_Eval, "opt_kwargs": dict(okw, options=xopts)}]
+    wheel = WheelSpinner(hub_dict, spokes)
+    wheel.spin(comm_world=Comm())
+    rec = {"strata_rank": wheel.strata_rank}
+    if wheel.strata_rank == 0:
+        rec.update(best_outer=wheel.BestOuterBound, best_inner=wheel.BestInnerBound,
+                   iters=wheel.spcomm.opt._PHIter, last_ib_idx=wheel.spcomm.last_ib_idx)
+    elif wheel.strata_rank == 2:
+        rec.update(tried=tried, best=wheel.spcomm.best_inner_bound)
+    out[rank] = rec
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_wheel_three_cylinders_gap(emu):
+    """PHHub + Lagrangian + x-bar spokes: the hub stops on rel_gap <= 1%; the
+    inner bound is the oracle's evaluation of x-bar (nonants fixed, LPs
+    re-solved) of the nonant vector it came from; outer <= EF <= inner."""
+    from oracle import models as om, ph as oph
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker3, args=(3, _free_port(), out), nprocs=3, join=True)
+    res = [out[r] for r in range(3)]
+    hub = [r for r in res if r["strata_rank"] == 0][0]
+    xs = [r for r in res if r["strata_rank"] == 2][0]
+    scens = [om.farmer("scen%d" % i, num_scens=S) for i in range(S)]
+    ef, _, _ = oph.solve_ef(scens)
+    assert hub["best_outer"] <= ef + 1e-6 * abs(ef) <= hub["best_inner"] + 2e-6 * abs(ef)
+    gap = (hub["best_inner"] - hub["best_outer"]) / abs(hub["best_outer"])
+    assert gap <= 0.01 and hub["iters"] < 200          # terminated on the gap, not the limit
+    assert hub["last_ib_idx"] == 2
+    # the spoke's evaluations, re-done by the oracle from the nonants it received
+    feas = [(v, b) for v, b in xs["tried"] if b is not None]
+    assert feas
+    for v, b in feas[:3] + feas[-2:]:
+        xb = v.reshape(S, -1).mean(axis=0)               # p = 1/S: x-bar of the ROOT node
+        E, _, ok = oph.evaluate_xhat(scens, {"ROOT": xb})
+        assert ok.all()
+        assert b == pytest.approx(E, rel=1e-8, abs=1e-6)
+    assert xs["best"] == pytest.approx(min(b for _, b in feas), rel=1e-12)
 
 
 def test_window_seqlock_roundtrip():
