@@ -325,6 +325,14 @@ typedef struct phx_iterk_result {
 int phx_iterk(phx_ctx* ctx, const phx_solve_opts* opts, const phx_iterk_args* args,
               phx_iterk_result* result_host, void* stream);
 
+/* Everything phx_iterk allocates or uploads for these arguments (segment
+ * tiles, control words, the mapped progress word, the fused mode's second
+ * output set, timing events), done ahead of the loop; no work is enqueued.
+ * Optional: phx_iterk does it itself on first use.  Replaces nothing in the
+ * reference (its loop has no device state); called where the reference
+ * builds its solver objects (SPOpt._create_solvers, spopt.py:839-903).      */
+int phx_iterk_prepare(phx_ctx* ctx, const phx_iterk_args* args);
+
 /* Human-readable state of the structure-specialised lane solver for this
  * context ("on: ..." or "off: <reason>").                                   */
 const char* phx_jit_info(const phx_ctx* ctx);

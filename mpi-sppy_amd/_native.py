@@ -96,7 +96,7 @@ class IterkResult(ctypes.Structure):
 SYMBOLS = [
     "create", "destroy", "last_error", "build_info", "set_problem", "set_bounds", "set_ph_terms",
     "solve", "solve_finish", "objective", "xbar", "update_w", "expect", "export_slots", "last_solve_stats", "jit_info",
-    "iterk",
+    "iterk", "iterk_prepare",
 ]
 
 
@@ -147,6 +147,7 @@ class Lib:
         self.jit_info = fn("jit_info", ctypes.c_char_p, [c_void_p])
         self.iterk = fn("iterk", ctypes.c_int, [c_void_p, ctypes.POINTER(SolveOpts), ctypes.POINTER(IterkArgs),
                                                 ctypes.POINTER(IterkResult), c_void_p])
+        self.iterk_prepare = fn("iterk_prepare", ctypes.c_int, [c_void_p, ctypes.POINTER(IterkArgs)])
 
     def check(self, ctx, rc, what):
         if rc != 0:

@@ -255,7 +255,19 @@ inline std::string lane_kernel_source(const LaneStructure& L, int warm_waves = 1
          "    phx_lane::compact_lane(still, sc, io.lanes_out, io.count_out);\n"
          "  }\n"
          "}\n";
+    // the cold solve: the interior point (phx_lane_cold), then over the same
+    // lanes the classification + active-set rounds (phx_lane_cold_as), which
+    // compacts what still needs the generic path (phx_lane.h ipm_lane)
     o << "extern \"C\" __global__ void __launch_bounds__(64) phx_lane_cold(phx_lane::LaneIO io, "
+         "const int* lanes, const int* count) {\n"
+         "  if (phx_lane::gated(io.gate)) return;\n"
+         "  const int nl = count ? *count : io.S;\n"
+         "  for (int base = blockIdx.x * 64; base < nl; base += gridDim.x * 64) {\n"
+         "    const int t = base + threadIdx.x;\n"
+         "    if (t < nl) phx_lane::ipm_lane<PT>(io, lanes ? lanes[t] : t);\n"
+         "  }\n"
+         "}\n";
+    o << "extern \"C\" __global__ void __launch_bounds__(64) phx_lane_cold_as(phx_lane::LaneIO io, "
          "const int* lanes, const int* count) {\n"
          "  if (phx_lane::gated(io.gate)) return;\n"
          "  phx_lane::zero_next_counts(io.counts_next);\n"
@@ -264,7 +276,7 @@ inline std::string lane_kernel_source(const LaneStructure& L, int warm_waves = 1
          "    const int t = base + threadIdx.x;\n"
          "    bool still = false;\n"
          "    int sc = -1;\n"
-         "    if (t < nl) { sc = lanes ? lanes[t] : t; still = phx_lane::cold_lane<PT>(io, sc); }\n"
+         "    if (t < nl) { sc = lanes ? lanes[t] : t; still = phx_lane::cold_rounds_lane<PT>(io, sc); }\n"
          "    phx_lane::compact_lane(still, sc, io.lanes_out, io.count_out);\n"
          "  }\n"
          "}\n";

@@ -158,6 +158,8 @@ struct LaneIO {
     double* y;
     double* x0;
     double* y0;
+    double* ipm_x;         // unscaled interior point [n*S] (phx_lane_cold -> phx_lane_cold_as)
+    double* ipm_y;         // [m*S]
     double* err;           // [S]
     int32_t* status;       // [S]: 1 certified, 0 running (generic path)
     int32_t* iters;        // [S]: IPM iterations used
@@ -309,6 +311,28 @@ PHX_LD double rsqrt_pos(double d) {
 #endif
 }
 
+// 1/d for the interior point's scalings (d != 0): on the GPU the hardware
+// reciprocal plus two Newton steps (a correctly rounded division is a
+// ~10-instruction dependent chain; the interior point needs no correct
+// rounding); rcp_step: one Newton step, for step-length ratios only.
+PHX_LD double rcp_fast(double d) {
+#if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC_RTC__)
+    double r = __builtin_amdgcn_rcp(d);
+    r = fma(r, fma(-d, r, 1.0), r);
+    return fma(r, fma(-d, r, 1.0), r);
+#else
+    return 1.0 / d;
+#endif
+}
+PHX_LD double rcp_step(double d) {
+#if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC_RTC__)
+    const double r = __builtin_amdgcn_rcp(d);
+    return fma(r, fma(-d, r, 1.0), r);
+#else
+    return 1.0 / d;
+#endif
+}
+
 // Packed Cholesky (lower, in place).  A pivot that collapses relative to its
 // original diagonal (a dependent row of A D A' near an interior-point
 // optimum) is replaced by a huge value, which zeroes that component of the
@@ -404,11 +428,38 @@ PHX_LD bool row_free(int i) { return !PT::blfin(i) && !PT::bufin(i); }
 // (da = affine step of the slack's variable, 0 in the predictor pass).
 // Returns the relative KKT error of (x, y); *its = iterations used.
 // ---------------------------------------------------------------------------
+// Hide a value's origin from the optimiser (no instruction): values derived
+// from it are recomputed where used instead of kept live across a loop.
+PHX_LD void opaque(double& v) {
+#if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC_RTC__)
+    __asm__ volatile("" : "+v"(v));
+#else
+    (void)v;
+#endif
+}
+
 PHX_LD double comp_lo(double sl, double r, double z, double smu, double da) {
     return smu - sl * z + da * z * (sl + da) * r;
 }
 PHX_LD double comp_up(double sl, double r, double z, double smu, double da) {
     return smu - sl * z + da * z * (da - sl) * r;
+}
+
+// the interior point's state, made opaque (only the entries that exist)
+template <class PT>
+PHX_LD void ipm_opaque(double* x, double* zl, double* zu, double* rl, double* ru, double* s, double* wl,
+                       double* wu, double* rwl, double* rwu, double* y) {
+    PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
+        opaque(x[j]);
+        if (has_lo<PT>(j)) { opaque(zl[j]); opaque(rl[j]); }
+        if (has_up<PT>(j)) { opaque(zu[j]); opaque(ru[j]); }
+    }
+    PHX_UNROLL for (int i = 0; i < PT::m(); ++i) {
+        opaque(y[i]);
+        if (!row_free<PT>(i) && !PT::eq(i)) opaque(s[i]);
+        if (row_lo<PT>(i)) { opaque(wl[i]); opaque(rwl[i]); }
+        if (row_up<PT>(i)) { opaque(wu[i]); opaque(rwu[i]); }
+    }
 }
 
 template <class PT>
@@ -460,14 +511,14 @@ PHX_LD double ipm_core(const Data<PT>& D, int max_it, double tol, double* x, dou
         double rl[NN], ru[NN], rwl[MM], rwu[MM];
         double mu = 0.0;
         PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
-            rl[j] = has_lo<PT>(j) ? 1.0 / (x[j] - D.l(j)) : 0.0;
-            ru[j] = has_up<PT>(j) ? 1.0 / (D.u(j) - x[j]) : 0.0;
+            rl[j] = has_lo<PT>(j) ? rcp_fast(x[j] - D.l(j)) : 0.0;
+            ru[j] = has_up<PT>(j) ? rcp_fast(D.u(j) - x[j]) : 0.0;
             if (has_lo<PT>(j)) mu += (x[j] - D.l(j)) * zl[j];
             if (has_up<PT>(j)) mu += (D.u(j) - x[j]) * zu[j];
         }
         PHX_UNROLL for (int i = 0; i < PT::m(); ++i) {
-            rwl[i] = row_lo<PT>(i) ? 1.0 / (s[i] - D.bl(i)) : 0.0;
-            rwu[i] = row_up<PT>(i) ? 1.0 / (D.bu(i) - s[i]) : 0.0;
+            rwl[i] = row_lo<PT>(i) ? rcp_fast(s[i] - D.bl(i)) : 0.0;
+            rwu[i] = row_up<PT>(i) ? rcp_fast(D.bu(i) - s[i]) : 0.0;
             if (row_lo<PT>(i)) mu += (s[i] - D.bl(i)) * wl[i];
             if (row_up<PT>(i)) mu += (D.bu(i) - s[i]) * wu[i];
         }
@@ -478,14 +529,14 @@ PHX_LD double ipm_core(const Data<PT>& D, int max_it, double tol, double* x, dou
             double h = D.p(j) + reg;
             if (has_lo<PT>(j)) h += zl[j] * rl[j];
             if (has_up<PT>(j)) h += zu[j] * ru[j];
-            Dx[j] = PT::fixed(j) ? 0.0 : 1.0 / h;
+            Dx[j] = PT::fixed(j) ? 0.0 : rcp_fast(h);
         }
         PHX_UNROLL for (int t = 0; t < TT; ++t) M[t] = 0.0;
         PHX_UNROLL for (int i = 0; i < PT::m(); ++i) {
             double sg = 0.0;
             if (row_lo<PT>(i)) sg += wl[i] * rwl[i];
             if (row_up<PT>(i)) sg += wu[i] * rwu[i];
-            isig[i] = (row_lo<PT>(i) || row_up<PT>(i)) ? 1.0 / sg : 0.0;
+            isig[i] = (row_lo<PT>(i) || row_up<PT>(i)) ? rcp_fast(sg) : 0.0;
             M[tri(i, i)] = row_free<PT>(i) ? 1.0 : (PT::eq(i) ? reg : isig[i] + reg);
         }
         PHX_UNROLL for (int t = 0; t < PT::npairs(); ++t) {
@@ -500,6 +551,7 @@ PHX_LD double ipm_core(const Data<PT>& D, int max_it, double tol, double* x, dou
         PHX_UNROLL for (int j = 0; j < PT::n(); ++j) dxa[j] = 0.0;
         PHX_UNROLL for (int i = 0; i < PT::m(); ++i) dsa[i] = 0.0;
         PHX_NOUNROLL for (int pass = 0; pass < 2; ++pass) {
+            ipm_opaque<PT>(x, zl, zu, rl, ru, s, wl, wu, rwl, rwu, y);
             {
                 double ax[MM], aty[NN];
                 D.matvec(x, ax);
@@ -543,6 +595,7 @@ PHX_LD double ipm_core(const Data<PT>& D, int max_it, double tol, double* x, dou
             }
             PHX_UNROLL for (int i = 0; i < PT::m(); ++i)
                 ds[i] = (PT::eq(i) || row_free<PT>(i)) ? 0.0 : (ds[i] - dy[i]) * isig[i];
+            ipm_opaque<PT>(x, zl, zu, rl, ru, s, wl, wu, rwl, rwu, y);
             // step lengths as inverse ratios (step = 1 / max(1, max ratio)),
             // multiplier steps recomputed from dx, ds
             double apr = 1.0, adr = 1.0;
@@ -551,13 +604,13 @@ PHX_LD double ipm_core(const Data<PT>& D, int max_it, double tol, double* x, dou
                     const double sl = x[j] - D.l(j);
                     const double dz = (comp_lo(sl, rl[j], zl[j], smu, dxa[j]) - zl[j] * dx[j]) * rl[j];
                     apr = fmax(apr, -dx[j] * rl[j]);
-                    adr = fmax(adr, -dz / zl[j]);
+                    adr = fmax(adr, -dz * rcp_step(zl[j]));
                 }
                 if (has_up<PT>(j)) {
                     const double sl = D.u(j) - x[j];
                     const double dz = (comp_up(sl, ru[j], zu[j], smu, dxa[j]) + zu[j] * dx[j]) * ru[j];
                     apr = fmax(apr, dx[j] * ru[j]);
-                    adr = fmax(adr, -dz / zu[j]);
+                    adr = fmax(adr, -dz * rcp_step(zu[j]));
                 }
             }
             PHX_UNROLL for (int i = 0; i < PT::m(); ++i) {
@@ -565,17 +618,17 @@ PHX_LD double ipm_core(const Data<PT>& D, int max_it, double tol, double* x, dou
                     const double sl = s[i] - D.bl(i);
                     const double dw = (comp_lo(sl, rwl[i], wl[i], smu, dsa[i]) - wl[i] * ds[i]) * rwl[i];
                     apr = fmax(apr, -ds[i] * rwl[i]);
-                    adr = fmax(adr, -dw / wl[i]);
+                    adr = fmax(adr, -dw * rcp_step(wl[i]));
                 }
                 if (row_up<PT>(i)) {
                     const double sl = D.bu(i) - s[i];
                     const double dw = (comp_up(sl, rwu[i], wu[i], smu, dsa[i]) + wu[i] * ds[i]) * rwu[i];
                     apr = fmax(apr, ds[i] * rwu[i]);
-                    adr = fmax(adr, -dw / wu[i]);
+                    adr = fmax(adr, -dw * rcp_step(wu[i]));
                 }
             }
-            ap = 1.0 / apr;
-            ad = 1.0 / adr;
+            ap = rcp_fast(apr);
+            ad = rcp_fast(adr);
             if (pass == 0) {
                 double maff = 0.0;
                 PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
@@ -935,12 +988,72 @@ PHX_LD bool map_apply(const Data<PT>& D, const LaneIO& io, int sc, double* xp, d
     return true;
 }
 
+// The largest violation among the flagged changes (kind * 64 + index; kinds:
+// 0/1 column to its lower/upper bound, 2 column freed, 3/4 row to its
+// lower/upper side, 5 row released): the largest relative primal violation,
+// else the largest wrong-signed multiplier.
+template <class PT, class CM>
+PHX_LD int worst_violation(const Data<PT>& D, CM enter_lo, CM enter_up, CM leave, uint32_t act_lo, uint32_t act_up,
+                           uint32_t drop, const double* xp, const double* z, double qmax) {
+    const double idt = 1.0 / (1.0 + qmax);
+    double bp = -1.0, bd = -1.0;
+    int kp = -1, kd = -1;
+    double atz[PT::NMAX_N], axp[PT::NMAX_M];
+    D.matvec_t(z, atz);
+    D.matvec(xp, axp);
+    PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
+        const double d = D.dc(j);
+        const double lam = (D.q(j) + D.p(j) * xp[j] + atz[j]) * D.idc(j);
+        if (PT::lfin(j)) {
+            const double v = (D.l(j) - xp[j]) * d * rcp_step(1.0 + fabs(D.l(j) * d));
+            const bool f = ((enter_lo >> j) & 1) && v > bp;
+            kp = f ? j : kp;
+            bp = f ? v : bp;
+        }
+        if (PT::ufin(j)) {
+            const double v = (xp[j] - D.u(j)) * d * rcp_step(1.0 + fabs(D.u(j) * d));
+            const bool f = ((enter_up >> j) & 1) && v > bp;
+            kp = f ? 64 + j : kp;
+            bp = f ? v : bp;
+        }
+        const double v = fabs(lam) * idt;
+        const bool f = ((leave >> j) & 1) && v > bd;
+        kd = f ? 128 + j : kd;
+        bd = f ? v : bd;
+    }
+    PHX_UNROLL for (int i = 0; i < PT::m(); ++i) {
+        const double id = D.idr(i);
+        if (PT::blfin(i)) {
+            const double v = (D.bl(i) - axp[i]) * id * rcp_step(1.0 + fabs(D.bl(i) * id));
+            const bool f = ((act_lo >> i) & 1u) && v > bp;
+            kp = f ? 192 + i : kp;
+            bp = f ? v : bp;
+        }
+        if (PT::bufin(i)) {
+            const double v = (axp[i] - D.bu(i)) * id * rcp_step(1.0 + fabs(D.bu(i) * id));
+            const bool f = ((act_up >> i) & 1u) && v > bp;
+            kp = f ? 256 + i : kp;
+            bp = f ? v : bp;
+        }
+        const double v = fabs(z[i] * D.dr(i)) * idt;
+        const bool f = ((drop >> i) & 1u) && v > bd;
+        kd = f ? 320 + i : kd;
+        bd = f ? v : bd;
+    }
+    return kp >= 0 ? kp : kd;
+}
+
 // KKT certificate of (xp, z) for active set a (unscaled, relative kkt_tol);
 // on failure applies the primal-dual active-set update (violated bounds/rows
 // enter, wrong-signed multipliers leave).  Returns 0 certified, 1 active set
 // changed, 2 not certified and nothing to change.
+// single: change only the worst violation (the largest relative primal
+// violation, else the largest wrong-signed multiplier) -- the anti-cycling
+// fallback of the later rounds: the full primal-dual update can cycle on
+// degenerate LP faces, one change at a time walks them like a pivot.
 template <class PT>
-PHX_LD int certify_update(const Data<PT>& D, ASet<PT>& a, const double* xp, const double* z, double kkt_tol) {
+PHX_LD int certify_update(const Data<PT>& D, ASet<PT>& a, const double* xp, const double* z, double kkt_tol,
+                          bool single = false) {
     typedef typename ASet<PT>::CMask CM;
     double qmax = 0.0;
     PHX_UNROLL for (int j = 0; j < PT::n(); ++j) qmax = fmax(qmax, fabs(D.q(j) * D.idc(j)));
@@ -992,23 +1105,40 @@ PHX_LD int certify_update(const Data<PT>& D, ASet<PT>& a, const double* xp, cons
         act_up |= (uint32_t)(!R && !below && above) << i;
         drop |= (uint32_t)dr << i;
     }
+    const bool changed = (enter_lo | enter_up | leave) != 0 || (act_lo | act_up | drop) != 0;
+    if (single && changed) {
+        // (the rare path: the violations' sizes are recomputed here so the
+        // common certificate carries none of this)
+        const int code = worst_violation<PT>(D, enter_lo, enter_up, leave, act_lo, act_up, drop, xp, z, qmax);
+        const int kind = code >> 6, ix = code & 63;
+        enter_lo = kind == 0 ? (CM)1 << ix : (CM)0;
+        enter_up = kind == 1 ? (CM)1 << ix : (CM)0;
+        leave = kind == 2 ? (CM)1 << ix : (CM)0;
+        act_lo = kind == 3 ? 1u << ix : 0u;
+        act_up = kind == 4 ? 1u << ix : 0u;
+        drop = kind == 5 ? 1u << ix : 0u;
+    }
     // primal-dual active-set update: violated bounds / rows enter, wrong-signed
     // multipliers leave
     a.f = (a.f & ~(enter_lo | enter_up)) | leave;
     a.u = (a.u & ~(enter_lo | leave)) | enter_up;
     a.r = (a.r | act_lo | act_up) & ~drop;
     a.l = (a.l & ~act_up) | act_lo;
-    const bool changed = (enter_lo | enter_up | leave) != 0 || (act_lo | act_up | drop) != 0;
     return changed ? 1 : (bad ? 2 : 0);
 }
 
-// KKT solve / certificate / active-set update rounds from (a, xp, z).
+// KKT solve / certificate / active-set update rounds from (a, xp, z): full
+// primal-dual updates for the first PHX_SINGLE_AFTER rounds, single changes
+// after (certify_update).
+#ifndef PHX_SINGLE_AFTER
+#define PHX_SINGLE_AFTER 1
+#endif
 template <class PT>
 PHX_LD bool as_rounds(const Data<PT>& D, ASet<PT>& a, const LaneIO& io, int rounds, double* xp, double* z) {
     PHX_NOUNROLL for (int r = 0; r < rounds; ++r) {
         PHX_LANE_STAT(0);
         if (!kkt_solve<PT>(D, a, xp, z)) return false;
-        const int c = certify_update<PT>(D, a, xp, z, io.kkt_tol);
+        const int c = certify_update<PT>(D, a, xp, z, io.kkt_tol, r >= PHX_SINGLE_AFTER);
         if (c == 0) return true;
         if (c == 2) { PHX_LANE_STAT(3); return false; }
     }
@@ -1097,15 +1227,38 @@ PHX_LD bool map_lane(const LaneIO& io, int sc) {
     return true;
 }
 
+// The cold solve is two kernels over the same lane list, so neither carries
+// the other's live state (together they needed ~740 registers per lane and
+// spilled to scratch on every IPM iteration):
+//   phx_lane_cold     ipm_lane: the interior point, stored (unscaled) with its
+//                     error and iteration count;
+//   phx_lane_cold_as  cold_rounds_lane: classify at that point, active-set
+//                     rounds, certificate; or the hand-off to the generic path.
 template <class PT>
-PHX_LD bool cold_lane(const LaneIO& io, int sc) {
+PHX_LD void ipm_lane(const LaneIO& io, int sc) {
+    constexpr int NN = PT::NMAX_N, MM = PT::NMAX_M;
+    const Data<PT> D(io, sc);
+    const int64_t S = io.S;
+    double x[NN], y[MM];
+    int its = 0;
+    const double err = ipm_core<PT>(D, io.max_it, io.ipm_tol, x, y, &its);
+    PHX_UNROLL for (int j = 0; j < PT::n(); ++j) io.ipm_x[j * S + sc] = x[j];
+    PHX_UNROLL for (int i = 0; i < PT::m(); ++i) io.ipm_y[i * S + sc] = y[i];
+    io.err[sc] = err;
+    io.iters[sc] = its;
+    io.flags[sc] = FLAG_IPM_TRIED;
+}
+
+template <class PT>
+PHX_LD bool cold_rounds_lane(const LaneIO& io, int sc) {
     constexpr int NN = PT::NMAX_N, MM = PT::NMAX_M;
     const Data<PT> D(io, sc);
     const int S = io.S;
     double x[NN], y[MM];
-    int its = 0;
-    const double err = ipm_core<PT>(D, io.max_it, io.ipm_tol, x, y, &its);
-    io.flags[sc] = FLAG_IPM_TRIED;
+    PHX_UNROLL for (int j = 0; j < PT::n(); ++j) x[j] = io.ipm_x[(int64_t)j * S + sc];
+    PHX_UNROLL for (int i = 0; i < PT::m(); ++i) y[i] = io.ipm_y[(int64_t)i * S + sc];
+    const double err = io.err[sc];
+    const int its = io.iters[sc];
     if (err < 1e-4) {
         ASet<PT> a;
         classify<PT>(D, x, y, fmin(1e-4, fmax(1e-9, 10.0 * err)), a);
@@ -1130,10 +1283,16 @@ PHX_LD bool cold_lane(const LaneIO& io, int sc) {
         const double v = PT::scaled() ? y[i] : y[i] * PT::idrs(i);
         io.yT[o] = v; io.y[o] = v; io.y0[o] = v;
     }
-    io.err[sc] = err;
-    io.iters[sc] = its;
     io.status[sc] = 0;
     return true;
+}
+
+// Both halves for one lane (the host emulation; the GPU runs them as two
+// kernels over the same list).  true: the lane needs the generic path.
+template <class PT>
+PHX_LD bool cold_lane(const LaneIO& io, int sc) {
+    ipm_lane<PT>(io, sc);
+    return cold_rounds_lane<PT>(io, sc);
 }
 
 #if defined(__HIPCC__) || defined(__HIPCC_RTC__)

@@ -51,6 +51,13 @@ class PHBase(SPOpt):
         self.conv = None
         self._PHIter = 0
         self.attach_xbars()
+        # the device loop's buffers and events, allocated with the problem
+        # (phx_iterk_prepare) so no PH iteration pays an allocation
+        if (self.batch.nonant.N > 0 and self.NNS > 0
+                and not self._native.jit_info(self._ctx).decode().startswith("off")):
+            lib = self._native
+            lib.check(self._ctx, lib.iterk_prepare(self._ctx, ctypes.byref(self._iterk_argstruct())),
+                      "iterk_prepare")
 
     # ------------------------------------------------------------ state
     def attach_xbars(self):
@@ -344,7 +351,7 @@ class PHBase(SPOpt):
         self.conv = None
         self.trivial_bound = self.Ebound(verbose)
         # per-scenario Iter0 optima (the outer bounds the trivial bound sums), on the device
-        self._iter0_obj_dev = self._obj.clone()
+        self._iter0_obj_dev.copy_(self._obj)
         if dprogress and self.cylinder_rank == 0:
             print("")
             print("After PH Iteration", self._PHIter)
@@ -372,7 +379,9 @@ class PHBase(SPOpt):
             return False
         if self.NNS == 0 or self.batch.nonant.N == 0:
             return False
-        return not self._native.jit_info(self._ctx).decode().startswith("off")
+        if getattr(self, "_jit_on", None) is None:
+            self._jit_on = not self._native.jit_info(self._ctx).decode().startswith("off")
+        return self._jit_on
 
     def _allreduce_cb(self):
         if getattr(self, "_ar_cb", None) is None:
@@ -412,6 +421,24 @@ class PHBase(SPOpt):
         so_dict = self.current_solver_options or {}
         so = self._solve_opts(so_dict)
         so.defer = 0
+        a = self._iterk_argstruct()
+        a.rho, a.W = self._rho.data_ptr(), self._W.data_ptr()
+        a.convthresh = float(self.options["convthresh"])
+        a.max_iters = int(max_iterations)
+        a.depth = int(so_dict.get("iterk_depth", 4))
+        a.timing = int(so_dict.get("iterk_timing", 0))
+        # fused mode (one launch per PH iteration, two-stage trees) unless
+        # {"iterk_fused": 0}; the library decides whether the problem allows it
+        a.node_stage_len = self._node_stage.numel() if int(so_dict.get("iterk_fused", 1)) else 0
+        res = _native.IterkResult()
+        t0 = time.perf_counter()
+        lib.check(self._ctx, lib.iterk(self._ctx, ctypes.byref(so), ctypes.byref(a), ctypes.byref(res),
+                                       self._stream()), "iterk")
+        return self._iterk_finish(res, time.perf_counter() - t0)
+
+    def _iterk_argstruct(self):
+        """phx_iterk_args over this object's device state (built once; W and rho
+        are set per call: PH_Prep re-creates them)."""
         a = getattr(self, "_iterk_args", None)
         if a is None:
             a = _native.IterkArgs()
@@ -430,20 +457,11 @@ class PHBase(SPOpt):
             a.conv_R = self._conv_R
             if self.n_proc > 1:
                 a.allreduce = self._allreduce_cb()
+            a.depth = 4
             self._iterk_args = a
-        a.rho, a.W = self._rho.data_ptr(), self._W.data_ptr()
-        a.convthresh = float(self.options["convthresh"])
-        a.max_iters = int(max_iterations)
-        a.depth = int(so_dict.get("iterk_depth", 4))
-        a.timing = int(so_dict.get("iterk_timing", 0))
-        # fused mode (one launch per PH iteration, two-stage trees) unless
-        # {"iterk_fused": 0}; the library decides whether the problem allows it
-        a.node_stage_len = self._node_stage.numel() if int(so_dict.get("iterk_fused", 1)) else 0
-        res = _native.IterkResult()
-        t0 = time.perf_counter()
-        lib.check(self._ctx, lib.iterk(self._ctx, ctypes.byref(so), ctypes.byref(a), ctypes.byref(res),
-                                       self._stream()), "iterk")
-        wall = time.perf_counter() - t0
+        return a
+
+    def _iterk_finish(self, res, wall):
         self._bump()
         self._PHIter = int(res.iters)
         self.conv = float(res.conv) if res.iters > 0 else None

@@ -303,6 +303,10 @@ class SPBase:
         self._x = torch.zeros(n * S, dtype=f64, device=self.device)
         self._y = torch.zeros(max(m, 1) * S, dtype=f64, device=self.device)
         self._obj = torch.zeros(S, dtype=f64, device=self.device)
+        self._iter0_obj_dev = torch.zeros(S, dtype=f64, device=self.device)   # Iter0's optima (PHBase)
+        # nonant slot -> column, and the original-nonant copy (SPOpt._save_original_nonants)
+        self._slot_cols_dev = torch.as_tensor(self.batch.nonant.slot_col.astype(np.int64), device=self.device)
+        self._orig_nonants_dev = torch.zeros((self.batch.nonant.N, S), dtype=f64, device=self.device)
         # the batched solve is exact (KKT-certified), so each scenario's outer
         # bound is its optimal objective (spopt.py:201-206): one buffer
         self._outer = self._obj
@@ -365,9 +369,14 @@ class SPBase:
         self._host_cache = {}
 
     def _stream(self):
-        if self.device.type == "cuda":
-            return torch.cuda.current_stream(self.device).cuda_stream
-        return None
+        """The stream every native call is ordered on: the device's current
+        stream when the object was built (its handle cached: looking it up
+        costs more than most kernel launches)."""
+        h = getattr(self, "_stream_h", None)
+        if h is None:
+            h = self._stream_h = (torch.cuda.current_stream(self.device).cuda_stream
+                                  if self.device.type == "cuda" else 0)
+        return h or None
 
     # ------------------------------------------------------------ host views
     def _bump(self):

@@ -263,30 +263,52 @@ class SPOpt(SPBase):
                                            self._stream()), "objective")
         self._bump()
 
+    def _expect_sums(self):
+        """[sum p*outer, sum p, sum p*[optimal]] over ALL ranks, on the host:
+        one all-reduce and one device->host copy per solve (Iter0's E1,
+        feas_prob and Ebound read the same three numbers)."""
+        buf = self._expect(self._outer)
+        key = self._expect_key
+        if getattr(self, "_expect_sums_key", None) != key:
+            R, r = self.n_proc, self.cylinder_rank
+            if R == 1:
+                v = buf[:3].cpu().numpy()
+            else:
+                # every rank's three sums side by side (x + 0 is exact), then
+                # summed in rank order on the host: the three totals see the
+                # same order, so E1 == E_feas exactly when every scenario is
+                # feasible (a ring all-reduce orders each element differently)
+                t = torch.zeros(3 * R, dtype=torch.float64, device=self.device)
+                t[3 * r:3 * r + 3] = buf[:3]
+                self.mpicomm.allreduce_(t)
+                parts = t.cpu().numpy().reshape(R, 3)
+                v = parts[0].copy()
+                for q in range(1, R):
+                    v = v + parts[q]
+            self._expect_sums_val = v
+            self._expect_sums_key = key
+        return self._expect_sums_val
+
+    def _pc0_all(self):
+        """sum over ranks of the local sum p * objective constant (once)."""
+        if getattr(self, "_pc0_sum", None) is None:
+            self._pc0_sum = float(self.mpicomm.allreduce_np([self._pc0])[0])
+        return self._pc0_sum
+
     def Ebound(self, verbose=False, extra_sum_terms=None):
         """sum_s p_s * outer_bound_s (+ extra terms), spopt.py:346-391."""
-        buf = self._expect(self._outer)
-        loc = [float(buf[0].item()) + self._pc0]
-        if extra_sum_terms is not None:
-            loc += list(extra_sum_terms)
-        t = torch.tensor(loc, dtype=torch.float64, device=self.device)
-        self.mpicomm.allreduce_(t)
+        v = float(self._expect_sums()[0]) + self._pc0_all()
         sgn = 1.0 if self.is_minimizing else -1.0
         if extra_sum_terms is None:
-            return sgn * float(t[0].item())
-        return sgn * float(t[0].item()), t[1:].cpu().numpy()
+            return sgn * v
+        extra = self.mpicomm.allreduce_np(np.asarray(list(extra_sum_terms), dtype=np.float64))
+        return sgn * v, extra
 
     def _update_E1(self):
-        buf = self._expect(self._outer)
-        t = buf[1:2].clone()
-        self.mpicomm.allreduce_(t)
-        self.E1 = float(t.item())
+        self.E1 = float(self._expect_sums()[1])
 
     def feas_prob(self):
-        buf = self._expect(self._outer)
-        t = buf[2:3].clone()
-        self.mpicomm.allreduce_(t)
-        return float(t.item())
+        return float(self._expect_sums()[2])
 
     def infeas_prob(self):
         buf = self._expect(self._outer)
@@ -423,29 +445,44 @@ class SPOpt(SPBase):
 
     def _save_original_nonants(self):
         """original_nonants / original_fixedness (spopt.py:690-710).  The values are
-        kept as a device copy (one gather, no host round trip inside Iter0);
-        ``original_nonants`` reads them back on first use."""
-        fixed, _ = self._fix_arrays()
+        kept as a device copy (one gather into a buffer allocated with the
+        problem: no allocation and no host round trip inside Iter0);
+        ``original_nonants`` reads them back on first use, and fixedness is
+        copied only when something was ever fixed."""
         self._settle()
         S = self._S
-        cols = torch.as_tensor(self.batch.nonant.slot_col.astype(np.int64), device=self.device)
-        self._orig_nonants_dev = self._x.view(-1, S)[cols].clone()
+        torch.index_select(self._x.view(-1, S), 0, self._slot_cols_dev, out=self._orig_nonants_dev)
+        self._orig_nonants_saved = True
         self._orig_nonants_host = None
-        self.original_fixedness = fixed.copy()
+        fixed = getattr(self, "_fixed", None)
+        self._orig_fixed = None if fixed is None else fixed.copy()   # None: nothing fixed
+        self._orig_fixed_saved = True
 
     @property
     def original_nonants(self):
         if getattr(self, "_orig_nonants_host", None) is None:
-            dev = getattr(self, "_orig_nonants_dev", None)
-            if dev is None:
+            if not getattr(self, "_orig_nonants_saved", False):
                 raise AttributeError("original_nonants: _save_original_nonants has not run")
-            self._orig_nonants_host = np.ascontiguousarray(dev.cpu().numpy().T)
+            self._orig_nonants_host = np.ascontiguousarray(self._orig_nonants_dev.cpu().numpy().T)
         return self._orig_nonants_host
 
     @original_nonants.setter
     def original_nonants(self, vals):
         self._orig_nonants_host = np.ascontiguousarray(np.asarray(vals, dtype=np.float64))
-        self._orig_nonants_dev = None
+        self._orig_nonants_saved = True
+
+    @property
+    def original_fixedness(self):
+        if not getattr(self, "_orig_fixed_saved", False):
+            return None
+        if self._orig_fixed is None:
+            self._orig_fixed = np.zeros((self._S, self.batch.nonant.N), dtype=bool)
+        return self._orig_fixed
+
+    @original_fixedness.setter
+    def original_fixedness(self, vals):
+        self._orig_fixed = None if vals is None else np.asarray(vals, dtype=bool).copy()
+        self._orig_fixed_saved = vals is not None
 
     def _restore_original_nonants(self):
         """spopt.py:713-741."""

@@ -4,6 +4,7 @@
 #   test:<pytest args>       e.g. "test:tests/test_netdes.py -k netdes50"
 #   bench:<tag>:<bench.py args>
 #   prof:<tag>:<bench.py args>          rocprofv3 --kernel-trace --stats
+#   trace:<tag>:<bench.py args>         rocprofv3 --kernel-trace --hip-runtime-trace (host gaps)
 #   pmc:<tag>:<counters>:<bench.py args> rocprofv3 --pmc (one pass; counters comma-separated)
 #   py:<tag>:<script and args>
 # Logs: gpurun_out/<tag>.log (tests: gpurun_out/test_<n>.log).
@@ -29,6 +30,11 @@ for step in "$@"; do
       tag="${rest%%:*}"; args="${rest#*:}"; log="gpurun_out/${tag}.log"
       echo "== step $n: rocprofv3 --kernel-trace --stats bench.py $args"
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "gpurun_out/${tag}" -o run -- python3 bench.py $args > "$log" 2>&1
+      rc=$?; tail -2 "$log" ;;
+    trace)
+      tag="${rest%%:*}"; args="${rest#*:}"; log="gpurun_out/${tag}.log"
+      echo "== step $n: rocprofv3 --kernel-trace --hip-runtime-trace bench.py $args"
+      timeout -k 10 600 rocprofv3 --kernel-trace --hip-runtime-trace -d "gpurun_out/${tag}" -o run -- python3 bench.py $args > "$log" 2>&1
       rc=$?; tail -2 "$log" ;;
     pmc)
       tag="${rest%%:*}"; rest2="${rest#*:}"; ctr="${rest2%%:*}"; args="${rest2#*:}"; log="gpurun_out/${tag}.log"

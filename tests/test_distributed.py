@@ -46,7 +46,7 @@ def _worker(rank, world, port, out, case):
                                         {"branching_factors": bfs, "start_seed": 0}, 3, lib=emu, device="cpu",
                                         mpicomm=Comm(), options=opts,
                                         all_nodenames=sputils.create_nodenames_from_branching_factors(bfs))
-    assert ph._iterk_args is not None if loop == "native" else not hasattr(ph, "_iterk_args")
+    assert hasattr(ph, "iterk_stats") if loop == "native" else not hasattr(ph, "iterk_stats")
     out[rank] = (conv, Eobj, tb, ph.W_array(), {k: v[0] for k, v in ph.xbar_by_node().items()})
     dist.barrier()
     dist.destroy_process_group()
