@@ -1302,6 +1302,18 @@ PHX_LD bool cold_lane(const LaneIO& io, int sc) {
 // workgroup whose add returns last reads with `sc1` loads after a barrier).
 // An agent release would write back the XCD L2 — the W stores of
 // k_update_w_seg included, several us — and the acquire invalidate L1.
+// The relaxed hand-off relies on gfx950's write-through agent-scope stores
+// (the guide's inter-workgroup visibility rule), which the HIP memory model
+// does not promise: any other target, or PHX_FENCED_HANDOFF (the parity tests
+// run it through PHX_LANE_DEFS), uses agent-scope release/acquire fences
+// around the arrival tickets instead.
+#if defined(PHX_FENCED_HANDOFF) || !defined(__gfx950__)
+#define PHX_HANDOFF_RELEASE() __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent")
+#define PHX_HANDOFF_ACQUIRE() __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent")
+#else
+#define PHX_HANDOFF_RELEASE() ((void)0)
+#define PHX_HANDOFF_ACQUIRE() ((void)0)
+#endif
 __device__ __forceinline__ void store_wt(double* p, double v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -1322,6 +1334,7 @@ __device__ bool arrive_last(unsigned int* tk, unsigned int nblocks) {
     __shared__ unsigned int s_last;
     if (threadIdx.x == 0) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        PHX_HANDOFF_RELEASE();
         const unsigned b = blockIdx.x, k = b % TICKET_SHARDS;
         const unsigned nk = (nblocks - k + TICKET_SHARDS - 1) / TICKET_SHARDS;   // blocks of shard k
         const unsigned nsh = nblocks < TICKET_SHARDS ? nblocks : TICKET_SHARDS;   // non-empty shards
@@ -1332,6 +1345,7 @@ __device__ bool arrive_last(unsigned int* tk, unsigned int nblocks) {
                                           __HIP_MEMORY_SCOPE_AGENT) == nsh - 1u;
         if (last)
             for (int q = 0; q <= TICKET_SHARDS; ++q) tk[q * TICKET_STRIDE] = 0u;
+        if (last) PHX_HANDOFF_ACQUIRE();
         s_last = last;
     }
     __syncthreads();
@@ -1443,11 +1457,13 @@ __device__ void fz_epilogue(const LaneIO& io, int sc, bool still, double dl) {
     if (threadIdx.x == 0) {
         PHX_UNROLL for (int e = 0; e < NV; ++e) store_wt(&f.part[(int64_t)b * NV + e], v[e]);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        PHX_HANDOFF_RELEASE();
         s_state = __hip_atomic_fetch_add(f.tk + k * TICKET_STRIDE, 1u, __ATOMIC_RELAXED,
                                          __HIP_MEMORY_SCOPE_AGENT) == nk - 1u;
     }
     __syncthreads();
     if (!s_state) return;
+    PHX_HANDOFF_ACQUIRE();
     // last of shard k: blocks k, k+8, ... in order (4 blocks' loads in flight)
     PHX_UNROLL for (int e = 0; e < NV; ++e) v[e] = 0.0;
     for (unsigned i0 = threadIdx.x; i0 < nk; i0 += 4 * 64) {
@@ -1465,6 +1481,7 @@ __device__ void fz_epilogue(const LaneIO& io, int sc, bool still, double dl) {
     if (threadIdx.x == 0) {
         PHX_UNROLL for (int e = 0; e < NV; ++e) store_wt(&shard_part[k * NV + e], v[e]);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        PHX_HANDOFF_RELEASE();
         const bool last = __hip_atomic_fetch_add(f.tk + TICKET_SHARDS * TICKET_STRIDE, 1u, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT) == nsh - 1u;
         if (last)
@@ -1473,6 +1490,7 @@ __device__ void fz_epilogue(const LaneIO& io, int sc, bool still, double dl) {
     }
     __syncthreads();
     if (s_state != 2u) return;
+    PHX_HANDOFF_ACQUIRE();
     // the last block overall: shards in order, then iteration k+1's stage
     const int e = threadIdx.x;
     if (e < NV) {

@@ -123,6 +123,8 @@ class PHBase(SPOpt):
                                           self._W.data_ptr(), W_out.data_ptr(), int(update), None,
                                           self._conv_R, self._seg_s0, self._seg_s1,
                                           self._seg_sums.data_ptr(), self._stream()), "update_w")
+        if update and self._prob0_mask_t is not None:
+            W_out.mul_(self._prob0_mask_t)     # zero-probability slots keep W = 0 (phbase.py:314-318)
         self._conv_cache = self._seg_sums      # consumed (all-reduced) by convergence_diff
         self._conv_value = None
         self._conv_updated_w = bool(update)
@@ -376,6 +378,8 @@ class PHBase(SPOpt):
         if not int(so.get("native_loop", 1)) or not int(self._solve_opts(so).lane_solver):
             return False
         if getattr(self, "_fixed", None) is not None and self._fixed.any():
+            return False
+        if self._prob0_mask_t is not None:      # W masked after every Update_W: the host loop
             return False
         if self.NNS == 0 or self.batch.nonant.N == 0:
             return False

@@ -18,6 +18,7 @@ single fused allreduce.
 """
 import ctypes
 import math
+import os
 import time
 import weakref
 
@@ -60,9 +61,10 @@ class SPBase:
             self._check_nodenames()
         else:
             raise RuntimeError("'ROOT' must be in the list of node names")
+        # per-variable probabilities (spbase.py:394-434): needs the per-scenario models
+        self.variable_probability = variable_probability
         if variable_probability is not None:
-            raise NotImplementedError("variable_probability is not supported by the batched engine")
-        self.variable_probability = None
+            self.options["per_scenario_models"] = True
         self.multistage = len(self.all_nodenames) > 1
         if mpicomm is None:
             # under torchrun (WORLD_SIZE > 1) join the process group: RCCL for GPU
@@ -93,6 +95,7 @@ class SPBase:
         self._set_sense()
         self._compute_unconditional_node_probabilities()
         self._attach_nonant_indices()
+        self._use_variable_probability_setter()
         self._create_communicators()
         self._upload_batch()
         self._spcomm = None
@@ -171,6 +174,76 @@ class SPBase:
             t = nn.slot_stage[j] - 1
             pc[j] = self.batch.prob / uncond[t]
         self._prob_coeff = pc
+
+    def _use_variable_probability_setter(self, verbose=False):
+        """Per-variable probabilities from ``variable_probability(model, **kw)``
+        -> [(id(var), prob)] (spbase.py:394-434): they replace the nonant slot's
+        prob_coeff for that scenario; a zero probability masks the slot's W
+        (prob0_mask, phbase.py:314-318).  Checked to sum to one per node and
+        variable unless options['do_not_check_variable_probabilities']."""
+        self._prob0_mask = None
+        self._has_variable_probability = self.variable_probability is not None
+        if self.variable_probability is None:
+            return
+        kw = self.options.get("variable_probability_kwargs", dict())
+        nn = self.batch.nonant
+        col_to_slot = {int(c): j for j, c in enumerate(nn.slot_col)}
+        mask = np.ones((nn.N, self.batch.S))
+        didit = 0
+        for s, sname in enumerate(self.local_scenario_names):
+            mdl = self._models[sname]
+            byid = {id(v): v for v in mdl._vars}
+            for vid, prob in self.variable_probability(mdl, **kw):
+                v = byid.get(vid)
+                if v is None or int(v.index) not in col_to_slot:
+                    raise KeyError(vid)       # the reference's varid_to_nonant_index lookup
+                j = col_to_slot[int(v.index)]
+                self._prob_coeff[j, s] = float(prob)
+                if prob == 0:
+                    mask[j, s] = 0.0
+                didit += 1
+        self._prob0_mask = mask
+        if verbose and self.cylinder_rank == 0:
+            print("variable_probability set", didit)
+        if not self.options.get("do_not_check_variable_probabilities", False):
+            self._check_variable_probabilities_sum(verbose)
+
+    def _check_variable_probabilities_sum(self, verbose=False):
+        """Per node and nonant: sum of the slot probabilities over scenarios == 1
+        (spbase.py:455-503)."""
+        nn = self.batch.nonant
+        loc = {}
+        for s in range(self.batch.S):
+            for j in range(nn.N):
+                key = (nn.node_of(nn.slot_stage[j] - 1, s), j)
+                loc[key] = loc.get(key, 0.0) + float(self._prob_coeff[j, s])
+        tot = {}
+        for d in self.mpicomm.allgather_object(loc):
+            for k, v in d.items():
+                tot[k] = tot.get(k, 0.0) + v
+        bad = {}
+        for (ndn, j), v in sorted(tot.items()):
+            if not np.isclose(v, 1.0, atol=self.E1_tolerance):
+                bad.setdefault(ndn, []).append((nn.var_names[j], v))
+        for ndn, lst in bad.items():
+            raise RuntimeError(f"Node {ndn}, variables {[a for a, _ in lst]} have respective"
+                               f" conditional probability sum {[b for _, b in lst]}"
+                               " which are not 1")
+
+    def is_zero_prob(self, scenario_model, var):
+        """spbase.py:436-452."""
+        if self.variable_probability is None:
+            return False
+        names = [k for k, m in (self._models or {}).items() if m is scenario_model]
+        if not names:
+            view = getattr(scenario_model, "_s", None)          # a ScenarioView
+            if view is None:
+                return False
+            s = view
+        else:
+            s = self.local_scenario_names.index(names[0])
+        j = list(self.batch.nonant.slot_col).index(var.index)
+        return float(self._prob_coeff[j, s]) == 0.0
 
     def _attach_nonant_indices(self):
         nn = self.batch.nonant
@@ -314,6 +387,8 @@ class SPBase:
         self._iters = torch.zeros(S, dtype=i32, device=self.device)
         self._prob = self._t(b.prob, f64)
         self._pc = self._t(self._prob_coeff.ravel(), f64)
+        self._prob0_mask_t = (None if getattr(self, "_prob0_mask", None) is None
+                              else self._t(self._prob0_mask.ravel(), f64))
         self._xbar_idx_t = self._t(self._xbar_idx.ravel(), i32)
         # [sum p x | sum p x^2] per (node, slot), all-reduced in place; xbar and
         # xsqbar are views of it (no copies per iteration)

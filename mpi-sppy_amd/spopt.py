@@ -52,6 +52,31 @@ SOLVER_DEFAULTS = {
 OPTIMAL, ITER_LIMIT, NUMERIC_FAIL, INFEASIBLE = 1, 2, 3, 4
 
 
+class SolveResults:
+    """What ``post_solve(s, results)`` hooks read from a solver results object
+    (spopt.py:166-206 hands Pyomo's to the extensions): ``solver.status``,
+    ``solver.termination_condition`` and ``problem.lower_bound/upper_bound``
+    (the subproblem's objective at the certified optimum, model sense)."""
+
+    class _NS:
+        pass
+
+    _TC = {OPTIMAL: "optimal", ITER_LIMIT: "maxIterations", NUMERIC_FAIL: "error", INFEASIBLE: "infeasible"}
+
+    def __init__(self, status, objective):
+        self.solver = SolveResults._NS()
+        self.problem = SolveResults._NS()
+        tc = SolveResults._TC.get(int(status), "unknown")
+        self.solver.termination_condition = tc
+        self.solver.status = "ok" if status == OPTIMAL else ("warning" if status == INFEASIBLE else "error")
+        ok = status == OPTIMAL
+        self.problem.lower_bound = float(objective) if ok else float("nan")
+        self.problem.upper_bound = float(objective) if ok else float("nan")
+
+    def __repr__(self):
+        return "SolveResults(%s, %r)" % (self.solver.termination_condition, self.problem.upper_bound)
+
+
 def _overrides(obj, name):
     """True if obj's class overrides hook ``name`` of its extension base."""
     from .extensions.extension import Extension
@@ -167,8 +192,12 @@ class SPOpt(SPBase):
             self._record_solve(rec, int(total.value), 0)
         if self.extensions is not None:
             if _overrides(self.extobject, "post_solve"):
-                for s in self.local_subproblems.values():
-                    self.extobject.post_solve(s, None)
+                self._settle()
+                stc = self._status.cpu().numpy()
+                sgn = 1.0 if self.is_minimizing else -1.0
+                objs = (self._obj.cpu().numpy() + self._c0_int) * sgn
+                for k, s in enumerate(self.local_subproblems.values()):
+                    self.extobject.post_solve(s, SolveResults(int(stc[k]), float(objs[k])))
             self.extobject.post_solve_loop()
         if dtiming:
             allt = self.mpicomm.gather(self.solve_stats[-1]["wall_s"])

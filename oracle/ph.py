@@ -125,6 +125,10 @@ class OraclePH:
 
     def update_w(self):
         self.W += self.rho * (self.xn() - self.xbar)
+        # variable probabilities: W of zero-probability nonants stays 0
+        # (phbase.py:314-318, prob0_mask from spbase.py:394-434)
+        if getattr(self, "prob0_mask", None) is not None:
+            self.W *= self.prob0_mask
 
     def convergence_diff(self):
         xn = self.xn()

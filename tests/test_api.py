@@ -183,3 +183,24 @@ def test_objective_constant_emu(emu):
     assert abs((E1 - E0) - shift) < 1e-9 * abs(E0) and abs((tb1 - tb0) - shift) < 1e-9 * abs(tb0)
     assert np.allclose(ph._host("obj") - base._host("obj"), [1000.0, 1010.0, 1020.0])
     assert conv1 == conv0
+
+
+def test_post_solve_gets_results(emu):
+    """post_solve(s, results) per subproblem (spopt.py:166-206): termination
+    condition and the subproblem objective (model sense) of the batched solve."""
+    class PS(Extension):
+        seen = []
+
+        def post_solve(self, s, results):
+            PS.seen.append((s.name, results.solver.termination_condition, results.problem.upper_bound))
+
+    PS.seen = []
+    ph = make(emu, iters=1, extensions=PS)
+    ph.ph_main()
+    S = len(ph.local_scenario_names)
+    assert len(PS.seen) == 2 * S                       # Iter0 + one iteration
+    assert all(tc == "optimal" for _, tc, _ in PS.seen)
+    last = {n: v for n, _, v in PS.seen[-S:]}
+    objs = ph._obj.cpu().numpy()
+    for k, n in enumerate(ph.local_scenario_names):
+        assert last[n] == pytest.approx(float(objs[k]), rel=1e-12)

@@ -329,3 +329,14 @@ def check_time_to_conv(lib, device, S):
 def test_time_to_conv_gpu(gpu_lib, S):
     ph = check_time_to_conv(gpu_lib, None, S)
     assert ph.iterk_stats["converged"]          # the device-driven loop ran the whole solve
+
+
+@pytest.mark.gpu
+def test_fenced_handoff_fused_loop_gpu(gpu_lib, monkeypatch):
+    """The fused loop's inter-workgroup hand-off with agent-scope release/acquire
+    fences (PHX_FENCED_HANDOFF, phx_lane.h) gives the host loop's trajectory,
+    as the default relaxed write-through hand-off does."""
+    monkeypatch.setenv("PHX_LANE_DEFS", "PHX_FENCED_HANDOFF")
+    from test_engine_emu import check_native_vs_host
+    a, b = check_native_vs_host(gpu_lib, None, "farmer", S=1000, fused=1)
+    assert a.iterk_stats["fused"]
