@@ -180,6 +180,7 @@ struct LaneIO {
     int32_t refine;
     int32_t as_rounds;     // active-set rounds after the interior point (phx_lane_cold)
     int32_t warm_rounds;   // active-set rounds per warm pass
+    int32_t single_after;  // rounds after which the active-set update changes one violation at a time
     const int32_t* gate;   // *gate != 0: the launch does nothing (phx_iterk past its stop), or null
     double* map;           // [map_words<PT>()][S] affine solution maps (see map_apply), or null
     FusedW fz;             // phx_iterk fused Update_W (fz.on = 0 otherwise)
@@ -1128,17 +1129,14 @@ PHX_LD int certify_update(const Data<PT>& D, ASet<PT>& a, const double* xp, cons
 }
 
 // KKT solve / certificate / active-set update rounds from (a, xp, z): full
-// primal-dual updates for the first PHX_SINGLE_AFTER rounds, single changes
+// primal-dual updates for the first io.single_after rounds, single changes
 // after (certify_update).
-#ifndef PHX_SINGLE_AFTER
-#define PHX_SINGLE_AFTER 1
-#endif
 template <class PT>
 PHX_LD bool as_rounds(const Data<PT>& D, ASet<PT>& a, const LaneIO& io, int rounds, double* xp, double* z) {
     PHX_NOUNROLL for (int r = 0; r < rounds; ++r) {
         PHX_LANE_STAT(0);
         if (!kkt_solve<PT>(D, a, xp, z)) return false;
-        const int c = certify_update<PT>(D, a, xp, z, io.kkt_tol, r >= PHX_SINGLE_AFTER);
+        const int c = certify_update<PT>(D, a, xp, z, io.kkt_tol, r >= io.single_after);
         if (c == 0) return true;
         if (c == 2) { PHX_LANE_STAT(3); return false; }
     }

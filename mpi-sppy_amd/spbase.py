@@ -347,6 +347,7 @@ class SPBase:
         # (_host obj/outer, Eobjective, Ebound, objs_dict), in the internal min sense
         self._c0_int = np.asarray(b.c0, dtype=np.float64) * sgn
         self._pc0 = math.fsum(float(p) * float(v) for p, v in zip(b.prob, self._c0_int))
+        self._pc0_sum = float(self.mpicomm.allreduce_np([self._pc0])[0])   # over ranks (Ebound / Eobjective)
         d = {}
         d["rowptr"] = self._t(b.rowptr, i32)
         d["colidx"] = self._t(b.colidx, i32)
