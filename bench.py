@@ -283,9 +283,11 @@ def main():
     # ---- warmup: a full untimed Iter0 + W iterations on its own object ----
     t = time.perf_counter()
     ph = make_ph(hl, S, cm, args.rho, so, args.warmup)
+    print("[bench] warmup object built (%.1f s)" % (time.perf_counter() - t), file=sys.stderr, flush=True)
     ph.ph_main(finalize=False)
     torch.cuda.synchronize()
     t_warm = time.perf_counter() - t
+    print("[bench] warmup done (%.1f s)" % t_warm, file=sys.stderr, flush=True)
     del ph
     # ---- timed: Iter0 + K iterations on a fresh object ----
     t = time.perf_counter()
@@ -293,6 +295,7 @@ def main():
     torch.cuda.synchronize()
     t_setup = time.perf_counter() - t
     T, T0, Tk = timed_run(ph, K)
+    print("[bench] timed run done (%.3f ms)" % (T * 1e3), file=sys.stderr, flush=True)
     st = getattr(ph, "iterk_stats", None)
     if st is not None and (st["iters"] != K or st["solves"] != K):
         raise RuntimeError("timed iterk_loop did not run %d full iterations: %s" % (K, st))

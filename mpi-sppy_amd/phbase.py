@@ -54,7 +54,7 @@ class PHBase(SPOpt):
         # the device loop's buffers and events, allocated with the problem
         # (phx_iterk_prepare) so no PH iteration pays an allocation
         if (self.batch.nonant.N > 0 and self.NNS > 0
-                and not self._native.jit_info(self._ctx).decode().startswith("off")):
+                and self._device_loop_solver(self._solve_opts(self.iterk_solver_options))):
             lib = self._native
             lib.check(self._ctx, lib.iterk_prepare(self._ctx, ctypes.byref(self._iterk_argstruct())),
                       "iterk_prepare")
@@ -375,7 +375,7 @@ class PHBase(SPOpt):
         if o["display_progress"] or o["verbose"] or o["display_convergence_detail"]:
             return False
         so = self.current_solver_options or {}
-        if not int(so.get("native_loop", 1)) or not int(self._solve_opts(so).lane_solver):
+        if not int(so.get("native_loop", 1)):
             return False
         if getattr(self, "_fixed", None) is not None and self._fixed.any():
             return False
@@ -383,9 +383,18 @@ class PHBase(SPOpt):
             return False
         if self.NNS == 0 or self.batch.nonant.N == 0:
             return False
-        if getattr(self, "_jit_on", None) is None:
-            self._jit_on = not self._native.jit_info(self._ctx).decode().startswith("off")
-        return self._jit_on
+        return self._device_loop_solver(self._solve_opts(so))
+
+    def _device_loop_solver(self, so):
+        """Which solve phx_iterk can run per iteration: the lane solver (jit on),
+        or, above its size limits, the workgroup warm pass (k_wg_warm)."""
+        info = getattr(self, "_jit_info", None)
+        if info is None:
+            info = self._jit_info = self._native.jit_info(self._ctx).decode()
+        if info.startswith("on") and int(so.lane_solver):
+            return True
+        return ("workgroup solver on" in info and int(so.wg_warm) > 0 and int(so.polish) > 0
+                and int(so.warm_start) > 0)
 
     def _allreduce_cb(self):
         if getattr(self, "_ar_cb", None) is None:

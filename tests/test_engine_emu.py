@@ -226,7 +226,7 @@ def test_farmer_cm10_workgroup_warm_pass(emu):
     kw = {"num_scens": S, "crops_multiplier": 10}
     res = {}
     for wg in (1, 0):
-        so = {"wg_warm": 16 * wg}
+        so = {"wg_warm": 16 * wg, "native_loop": 0}   # per-solve statistics: the host loop
         res[wg] = run_engine(farmer.scenario_creator, farmer.scenario_names_creator(S), kw, it, lib=emu,
                              device="cpu", options={"iter0_solver_options": so, "iterk_solver_options": so})
     ph1, ph0 = res[1][0], res[0][0]
@@ -264,3 +264,34 @@ def test_time_to_conv_emu(emu):
     import test_gpu_parity as tg
     ph = tg.check_time_to_conv(emu, "cpu", 3)
     assert ph._PHIter == 94
+
+
+def check_native_vs_host_wg(lib, device, S=20, iters=5, solver=None):
+    """Subproblems above the lane solver's limits (farmer crops_multiplier=10):
+    phx_iterk runs the workgroup warm pass per iteration (stragglers through
+    the stop / finish / resume protocol) == the host loop, bit for bit."""
+    runs = []
+    for nl in (1, 0):
+        so = dict(solver or {}, native_loop=nl)
+        opts = {"iter0_solver_options": dict(solver or {}), "iterk_solver_options": so}
+        runs.append(run_engine(farmer.scenario_creator, farmer.scenario_names_creator(S),
+                               {"num_scens": S, "crops_multiplier": 10}, iters, lib=lib, device=device,
+                               options=opts))
+    (a, ca, Ea, ta), (b, cb, Eb, tb_) = runs
+    assert hasattr(a, "iterk_stats") and not hasattr(b, "iterk_stats")
+    assert not a._native.jit_info(a._ctx).decode().startswith("on")
+    assert a._PHIter == b._PHIter
+    assert np.array_equal(a.W_array(), b.W_array())
+    assert np.array_equal(a.nonant_values(), b.nonant_values())
+    assert ca == cb and Ea == Eb and ta == tb_
+    return a, b
+
+
+def test_native_loop_workgroup_matches_host_loop_emu(emu):
+    check_native_vs_host_wg(emu, "cpu")
+
+
+def test_native_loop_workgroup_stragglers_emu(emu):
+    """One workgroup round per solve: lanes left to PDHG + polish stop the
+    device loop, which finishes them and resumes (same trajectory)."""
+    check_native_vs_host_wg(emu, "cpu", solver={"wg_warm": 1})   # (the stop count: GPU test)

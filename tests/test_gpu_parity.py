@@ -340,3 +340,19 @@ def test_fenced_handoff_fused_loop_gpu(gpu_lib, monkeypatch):
     from test_engine_emu import check_native_vs_host
     a, b = check_native_vs_host(gpu_lib, None, "farmer", S=1000, fused=1)
     assert a.iterk_stats["fused"]
+
+
+def test_native_loop_workgroup_matches_host_loop_gpu(gpu_lib):
+    """farmer crops_multiplier=10 x 1000 (configs[1]): phx_iterk runs the
+    workgroup warm pass per iteration, bit-equal to the host loop."""
+    from test_engine_emu import check_native_vs_host_wg
+    a, b = check_native_vs_host_wg(gpu_lib, None, S=1000, iters=6)
+    assert a.iterk_stats["not_optimal"] == 0
+
+
+def test_native_loop_workgroup_stragglers_gpu(gpu_lib):
+    """One workgroup round per solve: uncertified lanes stop the device loop,
+    which finishes them with PDHG + polish and resumes; same trajectory."""
+    from test_engine_emu import check_native_vs_host_wg
+    a, b = check_native_vs_host_wg(gpu_lib, None, S=300, iters=5, solver={"wg_warm": 1})
+    assert a.iterk_stats["straggler_stops"] > 0
