@@ -201,8 +201,12 @@ def dominant_kernel(ph, K, fused):
     b = ph.batch
     st = getattr(ph, "iterk_stats", None)
     if st is not None and st.get("warm_launches", 0) > 0:
-        return ("phx_lane_warm", st["lane_warm_ms"] / 1e3 / st["warm_launches"], st["warm_launches"],
-                lane_bytes(b, fused=bool(st.get("fused")) and fused), b.S)
+        # phx_iterk times its per-iteration solve kernel: the lane solver's warm
+        # launch, or (subproblems above the lane limits) the workgroup pass
+        if ph._native.jit_info(ph._ctx).decode().startswith("on"):
+            return ("phx_lane_warm", st["lane_warm_ms"] / 1e3 / st["warm_launches"], st["warm_launches"],
+                    lane_bytes(b, fused=bool(st.get("fused")) and fused), b.S)
+        return ("k_wg_warm", st["lane_warm_ms"] / 1e3 / st["warm_launches"], st["warm_launches"], wg_bytes(b), b.S)
     stats = ph.solve_stats[-K:]
     cand = {
         "phx_lane_warm": (sum(s.get("lane_warm_ms", 0.0) for s in stats), lane_bytes(b)),

@@ -107,6 +107,10 @@ typedef struct phx_solve_opts {
     int32_t sp_rounds;        /* sparse solver: active-set rounds after its
                                  interior point (cold) and from the previous
                                  solution (warm)                              */
+    int32_t seed_templates;   /* first solve of a context (Iter0) with the lane
+                                 solver: template lanes (interior point) whose
+                                 active sets the other lanes try in turn before
+                                 their own interior point (1..8)              */
 } phx_solve_opts;
 
 /* Statistics of the most recent phx_solve (HIP events on the solve stream). */

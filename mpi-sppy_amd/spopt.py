@@ -14,7 +14,7 @@ phbase.py:273-275): keys ``pdhg_max_iters``, ``pdhg_check_every``,
 ``pdhg_restart_max``, ``polish``, ``polish_refine``, ``polish_below``,
 ``kkt_tol``, ``opt_tol``, ``polish_reg``, ``warm_start``, ``ipm_after``,
 ``ipm_max_it``, ``ipm_tol``, ``lane_solver``, ``as_rounds``, ``warm_passes``, ``wg_warm``,
-``sp``, ``sp_rounds``.
+``sp``, ``sp_rounds``, ``seed_templates``.
 """
 import ctypes
 import inspect
@@ -47,6 +47,7 @@ SOLVER_DEFAULTS = {
     "wg_warm": 16,
     "sp": 1,
     "sp_rounds": 16,
+    "seed_templates": 1,
 }
 
 OPTIMAL, ITER_LIMIT, NUMERIC_FAIL, INFEASIBLE = 1, 2, 3, 4
@@ -139,6 +140,7 @@ class SPOpt(SPBase):
         so.wg_warm = int(o["wg_warm"])
         so.sp = int(o["sp"])
         so.sp_rounds = int(o["sp_rounds"])
+        so.seed_templates = int(o["seed_templates"])
         return so
 
     def _set_ph_terms(self):

@@ -47,3 +47,10 @@ def oracle_continue_from(ph_iter0, scens, iters, rho=1.0):
     o.W_on = o.prox_on = 1
     o.iterk(iters, 1e-10)
     return o
+
+
+def all_certified(ph):
+    """Every solve certified: the host loop's per-solve statistics and, when the
+    device loop (phx_iterk) ran the iterations, its count of uncertified lanes."""
+    return (all(s["not_optimal"] == 0 for s in ph.solve_stats)
+            and getattr(ph, "iterk_stats", {}).get("not_optimal", 0) == 0)

@@ -9,7 +9,7 @@ the farmer/aircond goldens (test_oracle_golden.py)."""
 import numpy as np
 import pytest
 
-from helpers import rel, run_engine
+from helpers import all_certified, rel, run_engine
 from mpisppy_amd.batch import from_models
 from mpisppy_amd.examples import netdes
 from oracle import models as om, ph as oph
@@ -72,7 +72,7 @@ def check_netdes_ph(lib, device, iters=3):
     o = oph.OraclePH([om.netdes(nm, INST) for nm in names], rho=1.0)
     otb = o.iter0()
     assert rel(tb, otb) < 1e-8
-    assert all(s["not_optimal"] == 0 for s in ph.solve_stats)
+    assert all_certified(ph)
     o.W = ph.W_array().copy()
     o.xbar = np.tile(ph.xbar_by_node()["ROOT"][0], (len(names), 1))
     o.W_on, o.prox_on = 1, 1
@@ -99,7 +99,7 @@ def test_netdes_synthetic_batch_gpu(gpu_lib):
     names = netdes.scenario_names_creator(200)
     ph, conv, Eobj, tb = run_engine(netdes.scenario_creator, names, {"instance": INST, "num_scens": 200}, 3,
                                     lib=gpu_lib)
-    assert all(s["not_optimal"] == 0 for s in ph.solve_stats)
+    assert all_certified(ph)
     pick = [0, 7, 10, 99, 199]
     o = oph.OraclePH([om.netdes(names[k], INST, num_scens=200) for k in pick], rho=1.0)
     o.iter0()
@@ -134,7 +134,7 @@ def check_netdes50(lib, device, S, iters, pick, solver=None):
         opts = {"iter0_solver_options": dict(solver), "iterk_solver_options": dict(solver)}
     ph, conv, Eobj, tb = run_engine(netdes.scenario_creator, names, kw, iters, lib=lib, device=device,
                                     options=opts)
-    assert all(s["not_optimal"] == 0 for s in ph.solve_stats), [s["not_optimal"] for s in ph.solve_stats]
+    assert all_certified(ph), [s["not_optimal"] for s in ph.solve_stats]
     o = oph.OraclePH([om.netdes(names[k], INST50, **okw) for k in pick], rho=1.0)
     o.iter0()
     # Iter0 objective per sampled scenario (unique LP optimum value)

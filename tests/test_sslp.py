@@ -7,7 +7,7 @@ whose PH loop is pinned by the farmer/aircond goldens (test_oracle_golden.py).""
 import numpy as np
 import pytest
 
-from helpers import rel, run_engine
+from helpers import all_certified, rel, run_engine
 from mpisppy_amd.batch import from_models
 from mpisppy_amd.examples import sslp
 from oracle import models as om, ph as oph
@@ -55,7 +55,7 @@ def check_sslp_ph(lib, device, iters=3):
     o = oph.OraclePH([om.sslp(nm, instance=5) for nm in names], rho=1.0)
     otb = o.iter0()
     assert rel(tb, otb) < 1e-8
-    assert all(s["not_optimal"] == 0 for s in ph.solve_stats)
+    assert all_certified(ph)
     o.W = ph.W_array().copy()
     xb = ph.xbar_by_node()["ROOT"][0]
     o.xbar = np.tile(xb, (len(names), 1))
@@ -79,7 +79,7 @@ def check_sslp_10k(lib, device, S, iters, pick):
     from the engine's own W / x-bar agree to 1e-8 / 1e-6 (nonants) / 1e-8 (obj)."""
     names = sslp.scenario_names_creator(S)
     ph, conv, Eobj, tb = run_engine(sslp.scenario_creator, names, {"num_scens": S}, iters, lib=lib, device=device)
-    assert all(s["not_optimal"] == 0 for s in ph.solve_stats), [s["not_optimal"] for s in ph.solve_stats]
+    assert all_certified(ph), [s["not_optimal"] for s in ph.solve_stats]
     o = oph.OraclePH([om.sslp(names[k], num_scens=S) for k in pick], rho=1.0)
     o.iter0()
     assert rel(ph._iter0_obj[pick], o.obj) < 1e-8
