@@ -438,6 +438,12 @@ PHX_LD void opaque(double& v) {
     (void)v;
 #endif
 }
+PHX_LD int opaque_index(int v) {
+#if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC_RTC__)
+    __asm__ volatile("" : "+v"(v));
+#endif
+    return v;
+}
 
 PHX_LD double comp_lo(double sl, double r, double z, double smu, double da) {
     return smu - sl * z + da * z * (sl + da) * r;
@@ -1131,10 +1137,16 @@ PHX_LD int certify_update(const Data<PT>& D, ASet<PT>& a, const double* xp, cons
 // KKT solve / certificate / active-set update rounds from (a, xp, z): full
 // primal-dual updates for the first io.single_after rounds, single changes
 // after (certify_update).
+// The lane's data (Data) is loaded afresh in every round, through an index the
+// optimiser cannot see through (opaque_index): loaded once before the loop, it
+// and the round's pair products / reciprocals hoisted with it stayed live
+// across the loop, spilled ~200 B of scratch per lane and doubled the warm
+// kernel's memory traffic; re-read, it comes from L2.
 template <class PT>
-PHX_LD bool as_rounds(const Data<PT>& D, ASet<PT>& a, const LaneIO& io, int rounds, double* xp, double* z) {
+PHX_LD bool as_rounds(const LaneIO& io, int sc, ASet<PT>& a, int rounds, double* xp, double* z) {
     PHX_NOUNROLL for (int r = 0; r < rounds; ++r) {
         PHX_LANE_STAT(0);
+        const Data<PT> D(io, opaque_index(sc));
         if (!kkt_solve<PT>(D, a, xp, z)) return false;
         const int c = certify_update<PT>(D, a, xp, z, io.kkt_tol, r >= io.single_after);
         if (c == 0) return true;
@@ -1188,9 +1200,10 @@ PHX_LD bool warm_lane(const LaneIO& io, int sc) {
         }
         // the active set moved: rounds from the updated set, warm from (xp, z)
     }
-    if (as_rounds<PT>(D, a, io, io.warm_rounds, xp, z)) {
-        const bool mok = MAP && io.map && map_compute<PT>(D, a, io, sc);
-        write_certified<PT>(io, D, sc, a, xp, z, 0, mok);
+    if (as_rounds<PT>(io, sc, a, io.warm_rounds, xp, z)) {
+        const Data<PT> Dc(io, opaque_index(sc));
+        const bool mok = MAP && io.map && map_compute<PT>(Dc, a, io, sc);
+        write_certified<PT>(io, Dc, sc, a, xp, z, 0, mok);
         return false;
     }
     aset_store<PT>(io, sc, a);   // the updated active set seeds the next pass
@@ -1250,7 +1263,6 @@ PHX_LD void ipm_lane(const LaneIO& io, int sc) {
 template <class PT>
 PHX_LD bool cold_rounds_lane(const LaneIO& io, int sc) {
     constexpr int NN = PT::NMAX_N, MM = PT::NMAX_M;
-    const Data<PT> D(io, sc);
     const int S = io.S;
     double x[NN], y[MM];
     PHX_UNROLL for (int j = 0; j < PT::n(); ++j) x[j] = io.ipm_x[(int64_t)j * S + sc];
@@ -1259,11 +1271,15 @@ PHX_LD bool cold_rounds_lane(const LaneIO& io, int sc) {
     const int its = io.iters[sc];
     if (err < 1e-4) {
         ASet<PT> a;
-        classify<PT>(D, x, y, fmin(1e-4, fmax(1e-9, 10.0 * err)), a);
+        {
+            const Data<PT> D(io, sc);
+            classify<PT>(D, x, y, fmin(1e-4, fmax(1e-9, 10.0 * err)), a);
+        }
         double xp[NN], z[MM];
         PHX_UNROLL for (int j = 0; j < PT::n(); ++j) xp[j] = x[j];
         PHX_UNROLL for (int i = 0; i < PT::m(); ++i) z[i] = a.R(i) ? -y[i] : 0.0;
-        if (as_rounds<PT>(D, a, io, io.as_rounds, xp, z)) {
+        if (as_rounds<PT>(io, sc, a, io.as_rounds, xp, z)) {
+            const Data<PT> D(io, opaque_index(sc));
             const bool mok = io.map && map_compute<PT>(D, a, io, sc);
             write_certified<PT>(io, D, sc, a, xp, z, its > 0 ? its : 1, mok);
             return false;
