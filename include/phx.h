@@ -111,6 +111,10 @@ typedef struct phx_solve_opts {
                                  solver: template lanes (interior point) whose
                                  active sets the other lanes try in turn before
                                  their own interior point (1..8)              */
+    int32_t rescue_rounds;    /* lane solver: active-set rounds (single changes)
+                                 of the rescue pass before any interior point,
+                                 and of the first warm pass after a cold solve;
+                                 0: max(16, 8 as_rounds)                      */
 } phx_solve_opts;
 
 /* Statistics of the most recent phx_solve (HIP events on the solve stream). */

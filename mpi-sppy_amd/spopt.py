@@ -14,7 +14,7 @@ phbase.py:273-275): keys ``pdhg_max_iters``, ``pdhg_check_every``,
 ``pdhg_restart_max``, ``polish``, ``polish_refine``, ``polish_below``,
 ``kkt_tol``, ``opt_tol``, ``polish_reg``, ``warm_start``, ``ipm_after``,
 ``ipm_max_it``, ``ipm_tol``, ``lane_solver``, ``as_rounds``, ``warm_passes``, ``wg_warm``,
-``sp``, ``sp_rounds``, ``seed_templates``.
+``sp``, ``sp_rounds``, ``seed_templates``, ``rescue_rounds``.
 """
 import ctypes
 import inspect
@@ -48,6 +48,7 @@ SOLVER_DEFAULTS = {
     "sp": 1,
     "sp_rounds": 16,
     "seed_templates": 1,
+    "rescue_rounds": 0,
 }
 
 OPTIMAL, ITER_LIMIT, NUMERIC_FAIL, INFEASIBLE = 1, 2, 3, 4
@@ -141,6 +142,7 @@ class SPOpt(SPBase):
         so.sp = int(o["sp"])
         so.sp_rounds = int(o["sp_rounds"])
         so.seed_templates = int(o["seed_templates"])
+        so.rescue_rounds = int(o["rescue_rounds"])
         return so
 
     def _set_ph_terms(self):

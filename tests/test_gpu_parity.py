@@ -189,8 +189,8 @@ def test_native_loop_fused_matches_host_loop_gpu(gpu_lib, case):
     check_native_vs_host(gpu_lib, None, case, S=1000, fused=1)
 
 
-@pytest.mark.parametrize("so,fused", [({"as_rounds": 0, "ipm_max_it": 2}, 0), ({"as_rounds": 1, "ipm_max_it": 3}, 0),
-                                      ({"as_rounds": 1, "ipm_max_it": 3}, 1)])
+@pytest.mark.parametrize("so,fused", [({"as_rounds": 0, "ipm_max_it": 2}, 0), ({"as_rounds": 1, "ipm_max_it": 3, "rescue_rounds": 1}, 0),
+                                      ({"as_rounds": 1, "ipm_max_it": 3, "rescue_rounds": 1}, 1)])
 def test_native_loop_straggler_stops_gpu(gpu_lib, so, fused):
     """Starved lane solves leave lanes to the generic path: phx_iterk stops the
     pipeline, finishes them and resumes; the trajectory equals the host loop's."""
