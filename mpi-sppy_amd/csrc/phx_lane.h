@@ -85,7 +85,10 @@ PHX_LD constexpr int aset_words(int n, int m) { return (2 * (n + m) + 31) / 32; 
 // Active-set KKT solves: quasi-definite regularisation and the cap on its
 // iterative-refinement steps (compile-time, so the refinement is unrolled and
 // 1/(p+reg) of the LP columns folds to a constant).
-constexpr double KKT_REG = 1e-6;
+#ifndef PHX_KKT_REG
+#define PHX_KKT_REG 1e-6
+#endif
+constexpr double KKT_REG = PHX_KKT_REG;
 constexpr int KKT_REFINE = 6;
 #ifndef PHX_KKT_STOP
 #define PHX_KKT_STOP 1e-10
