@@ -107,6 +107,11 @@ def sp_bytes(b):
     return rd + wr
 
 
+# profiles/r*_pmc_<tag>_<kernel>.json of each secondary config (scripts/pmc_summary.py
+# over the config's timed launches)
+CONFIG_PMC_TAG = {"C2": "farmercm10_1k", "C4": "aircond1k", "C5a": "sslp10k", "C5b": "netdes10k"}
+
+
 def pmc_traffic(kernel, tag):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
     (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; scripts/pmc_summary.py): counters
@@ -253,7 +258,8 @@ def run_config(name, w, args, K, so, world):
            "nonants": ph.batch.nonant.N, "steps": K,
            "value": S * (K + 1) / T, "unit": "scenario-iterations/s", "T_s": T, "iter0_s": T0,
            "steady": {"value": S * K / Tk, "ms_per_step": Tk * 1e3 / K},
-           "roofline": roofline(kernel, avg_s, launches, bpu, units),
+           "roofline": roofline(kernel, avg_s, launches, bpu, units,
+                                *pmc_traffic(kernel, CONFIG_PMC_TAG.get(name, name))),
            "solver": ph._native.jit_info(ph._ctx).decode(), "not_optimal": nbad, "setup_s": setup,
            "loop": "phx_iterk (device-driven)" if st is not None else "PHBase host loop (deferred solves)"}
     if w.get("cpu") and not args.no_cpu_baseline:
@@ -305,8 +311,12 @@ def main():
         raise RuntimeError("timed iterk_loop did not run %d full iterations: %s" % (K, st))
     kernel, avg_s, launches, bpu, units = dominant_kernel(ph, K, args.fused)
     b = ph.batch
-    traffic, tsrc = (pmc_traffic(kernel, "farmer100k") if world == 1 and args.only is None and S == 100000
-                     and cm == 1 else (None, None))
+    if world != 1:
+        traffic, tsrc = None, None
+    elif args.only is not None:
+        traffic, tsrc = pmc_traffic(kernel, CONFIG_PMC_TAG.get(args.only, args.only))
+    else:
+        traffic, tsrc = (pmc_traffic(kernel, "farmer100k") if S == 100000 and cm == 1 else (None, None))
     nbad = sum(s.get("not_optimal", 0) for s in ph.solve_stats) + (st.get("not_optimal", 0) if st else 0)
     res = {
         "metric": "PH scenario-iterations/sec (farmer 100k) + time to conv<1e-4",
