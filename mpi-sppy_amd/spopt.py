@@ -305,7 +305,7 @@ class SPOpt(SPBase):
         if getattr(self, "_expect_sums_key", None) != key:
             R, r = self.n_proc, self.cylinder_rank
             if R == 1:
-                v = buf[:3].cpu().numpy()
+                v = self._read_small(buf[:3])
             else:
                 # every rank's three sums side by side (x + 0 is exact), then
                 # summed in rank order on the host: the three totals see the
