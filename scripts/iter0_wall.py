@@ -48,6 +48,12 @@ def _init(self, *a, **k):
 
 
 _native.Lib.__init__ = _init
+import gc  # noqa: E402
+GC = []
+gc.callbacks.append(lambda phase, info: GC.append((time.perf_counter(), phase, info.get("generation"))))
+if os.environ.get("GC_FREEZE"):
+    gc.collect()
+    gc.freeze()
 S = int(os.environ.get("SCENS", "100000"))
 w = {"names": farmer.scenario_names_creator, "creator": farmer.scenario_creator,
      "kw": lambda S, cm: {"num_scens": S, "crops_multiplier": cm}, "nodes": None}
@@ -55,6 +61,7 @@ for rep in range(2):
     ph = bench.make_ph(w, S, 1, 1.0, {}, 20)
     torch.cuda.synchronize()
     REC.clear()
+    GC.clear()
     T = bench.timed_run(ph, 20)
     print("run", rep, "T, T_iter0, T_iterk (ms):", ["%.3f" % (1e3 * v) for v in T])
     del ph
@@ -62,3 +69,6 @@ t_first = min(r[0] for r in REC if r[3].endswith("Iter0"))
 for t0, t1, d, name in sorted(REC):
     if t0 >= t_first - 1e-3:
         print("%9.1f %9.1f  %s%s" % ((t0 - t_first) * 1e6, (t1 - t0) * 1e6, "  " * d, name))
+gcs = [g for g in GC if g[0] >= t_first - 1e-3]
+for (ta, pa, ga), (tb, pb, gb) in zip(gcs[::2], gcs[1::2]):
+    print("%9.1f %9.1f  gc generation %s" % ((ta - t_first) * 1e6, (tb - ta) * 1e6, ga))

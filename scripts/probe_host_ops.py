@@ -39,3 +39,25 @@ def pinned():
 
 t("pinned copy + stream sync", pinned)
 t("current_stream().cuda_stream", lambda: torch.cuda.current_stream(dev).cuda_stream)
+
+# the same reads right after a large write (dirty caches, as after Iter0's solve)
+big = torch.empty(25_000_000, dtype=torch.float64, device=dev)
+
+
+def after_big(f):
+    def g():
+        big.fill_(1.0)
+        st.synchronize()
+        t0 = time.perf_counter()
+        big[:3].add_(1.0)                     # a tiny kernel behind it (k_expect's place)
+        f()
+        return time.perf_counter() - t0
+    return g
+
+
+for name, f in (("pageable .cpu()", lambda: buf[:3].cpu().numpy()), ("pinned copy + sync", pinned),
+                ("stream sync only", lambda: st.synchronize())):
+    g = after_big(f)
+    g()
+    ts = [g() for _ in range(20)]
+    print("after 200 MB write: %-28s %8.1f us" % (name, 1e6 * sum(ts) / len(ts)), flush=True)
