@@ -162,6 +162,11 @@ def workloads():
         "C5a": dict(creator=sslp.scenario_creator, names=lambda S: sslp.scenario_names_creator(10000),
                     kw=lambda S, cm: {"num_scens": 10000}, nodes=None, S=10000,
                     desc="sslp_15_45 LP relaxation, 10,000 stochastic-RHS scenarios (BASELINE configs[4])",
+                    # a few sslp lanes need the sparse interior point in every PH
+                    # iteration anyway: more workgroup rounds only delay them
+                    # (measured: 16 rounds 24.4, 8 18.9, 4 16.3 ms per iteration;
+                    # profiles/r02_s18_wg_rounds.txt)
+                    so={"wg_warm": 4},
                     cpu=dict(model="sslp", scens=128, iters=1, total=10000)),
         "C5b": dict(creator=netdes.scenario_creator, names=lambda S: netdes.scenario_names_creator(10000),
                     kw=lambda S, cm: {"instance": "network-50-30-H-01", "num_scens": 10000}, nodes=None, S=10000,
@@ -244,6 +249,7 @@ def roofline(kernel, avg_s, launches, bpu, units, traffic=None, traffic_src=None
 def run_config(name, w, args, K, so, world):
     """One secondary config at N = 1: Iter0 + K iterations on a fresh PH object."""
     S = w["S"]
+    so = dict(so, **w.get("so", {}))
     t = time.perf_counter()
     ph = make_ph(w, S, 1, args.rho, so, K)
     torch.cuda.synchronize()
@@ -261,7 +267,8 @@ def run_config(name, w, args, K, so, world):
            "roofline": roofline(kernel, avg_s, launches, bpu, units,
                                 *pmc_traffic(kernel, CONFIG_PMC_TAG.get(name, name))),
            "solver": ph._native.jit_info(ph._ctx).decode(), "not_optimal": nbad, "setup_s": setup,
-           "loop": "phx_iterk (device-driven)" if st is not None else "PHBase host loop (deferred solves)"}
+           "loop": "phx_iterk (device-driven)" if st is not None else "PHBase host loop (deferred solves)",
+           "solver_options": w.get("so", {})}
     if w.get("cpu") and not args.no_cpu_baseline:
         c = w["cpu"]
         res["cpu_baseline"] = cpu_baseline(args, model=c["model"], cm=c.get("cm", 1), scens=c["scens"],
@@ -288,6 +295,7 @@ def main():
     so = {"lane_solver": args.lane_solver, "iterk_depth": args.depth, "iterk_timing": args.timing_every,
           "iterk_fused": args.fused}
     hl = W["C3"] if args.only is None else W[args.only]
+    so.update(hl.get("so", {}))
     S = args.scens if args.only is None else hl["S"]
     cm = args.cm if args.only is None else 1
     # ---- warmup: a full untimed Iter0 + W iterations on its own object ----
