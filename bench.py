@@ -124,6 +124,31 @@ def pmc_traffic(kernel, tag):
     return d.get("hbm_bytes_per_launch", {}).get("total"), os.path.relpath(files[-1], _ROOT)
 
 
+def valu_issue(kernel, tag, units, avg_s, lanes_per_wave=64, simds=1024, clock_hz=2.4e9):
+    """The kernel's VALU-issue roofline from the committed SQ counter pass
+    (profiles/r*_pmcsq_<tag>_<kernel>.json, same command, timed launches):
+    SQ_INSTS_VALU wave-instructions per launch spread over the launch's
+    wavefronts; the busiest SIMD holds ceil(waves / 1,024) of them, and a wave64
+    VALU instruction issues in 4 cycles on a 16-lane SIMD (MI355X_MICROARCH.md:
+    1,024 SIMDs, 2,400 MHz) -- the time the kernel would take if it issued a VALU
+    instruction every cycle it could."""
+    import glob
+    files = sorted(glob.glob(os.path.join(_ROOT, "profiles", "r*_pmcsq_%s_%s.json" % (tag, kernel))))
+    if not files or not avg_s:
+        return None
+    d = json.load(open(files[-1]))
+    insts = d.get("counters", {}).get("SQ_INSTS_VALU")
+    if not insts:
+        return None
+    waves = -(-units // lanes_per_wave)
+    per_wave = insts / waves
+    busiest = -(-waves // simds)
+    bound_s = busiest * per_wave * 4 / clock_hz
+    return {"valu_insts_per_launch": insts, "valu_insts_per_wave": per_wave, "waves_per_launch": waves,
+            "busiest_simd_waves": busiest, "issue_bound_us": bound_s * 1e6, "frac": bound_s / avg_s,
+            "source": os.path.relpath(files[-1], _ROOT)}
+
+
 def cpu_baseline(args, model="farmer", cm=1, scens=None, iters=None, total=None, timeout=900):
     """oracle/cpu_bench.py in a child process (it never touches the GPU)."""
     procs = max(1, min(args.cpu_procs, os.cpu_count() or 1))
@@ -191,15 +216,20 @@ def timed_run(ph, K):
     ph.options["PHIterLimit"] = K
     ph.mpicomm.Barrier()
     torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     t0 = time.perf_counter()
+    ev[0].record()
     ph.Iter0()
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
+    # (no synchronize between Iter0 and iterk_loop -- ph_main has none: the
+    # Iter0 share is the device time between two events on the same stream,
+    # its last work included)
+    ev[1].record()
     ph.iterk_loop()
     ph._settle()
     torch.cuda.synchronize()
     ph.mpicomm.Barrier()
     t2 = time.perf_counter()
+    t1 = t0 + ev[0].elapsed_time(ev[1]) / 1e3
     tt = torch.tensor([t2 - t0, t1 - t0, t2 - t1], dtype=torch.float64, device="cuda")
     ph.mpicomm.allreduce_max_(tt)
     return [float(v) for v in tt.cpu()]
@@ -346,7 +376,9 @@ def main():
                    "parallelism": "scenario-sharded x%d, RCCL allreduce" % world},
         "T_s": T, "iter0_s": T0,
         "steady": {"value": S * K / Tk, "ms_per_step": Tk * 1e3 / K, "def": "S K / T_iterk (Iter0 excluded)"},
-        "roofline": roofline(kernel, avg_s, launches, bpu, units, traffic, tsrc),
+        "roofline": dict(roofline(kernel, avg_s, launches, bpu, units, traffic, tsrc),
+                         valu=valu_issue(kernel, "farmer100k", units, avg_s)
+                         if (world == 1 and args.only is None and S == 100000 and cm == 1) else None),
         "loop": ("PHBase.iterk_loop -> phx_iterk (device-driven, depth %d%s)"
                  % (args.depth, ", fused" if st and st.get("fused") else "")) if st else "PHBase host loop",
         "not_optimal": nbad, "setup_s": t_setup, "warmup_s": t_warm,
