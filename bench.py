@@ -12,7 +12,8 @@ it fits one MI355X), rho = 1, scenarios sharded contiguously over the ranks
 
 Metric: value = S (K + 1) / T, T = wall time of Iter0 + K PH
 iterations (PHBase.Iter0 then PHBase.iterk_loop with PHIterLimit = K, on the
-device: phx_iterk), bracketed by barrier + device synchronize, MAX over ranks; K
+device: phx_iterk), bracketed by barrier + device synchronize (none in between:
+Iter0's share from events around it), MAX over ranks; K
 steps are timed, Iter0 counts as one more scenario-solve pass.  W warmup: a full
 untimed Iter0 + W iterations on a separate PH object first (JIT, allocator).
 Inputs resident in HBM before timing.  Extra keys:
