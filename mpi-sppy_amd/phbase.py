@@ -325,8 +325,14 @@ class PHBase(SPOpt):
         self._PHIter = 0
         self._create_solvers()
         teeme = bool(self.options.get("tee-rank0-solves", False)) and self.cylinder_rank == 0
-        self.solve_loop(solver_options=self.current_solver_options, dtiming=dtiming, gripe=True,
-                        tee=teeme, verbose=verbose)
+        # E1 / feas_prob / Ebound read their sums behind the solve's own wait
+        # (SPOpt._expect_ahead)
+        self._expect_ahead_wanted = True
+        try:
+            self.solve_loop(solver_options=self.current_solver_options, dtiming=dtiming, gripe=True,
+                            tee=teeme, verbose=verbose)
+        finally:
+            self._expect_ahead_wanted = False
         self._update_E1()
         if abs(1 - self.E1) > self.E1_tolerance:
             if self.cylinder_rank == 0:

@@ -454,6 +454,13 @@ class SPBase:
                                   if self.device.type == "cuda" else 0)
         return h or None
 
+    def _pinned_small(self):
+        """64 pinned host doubles, allocated once (small device reads)."""
+        pin = getattr(self, "_pin_small", None)
+        if pin is None:
+            pin = self._pin_small = torch.empty(64, dtype=torch.float64, pin_memory=True)
+        return pin
+
     def _read_small(self, t):
         """A few device doubles on the host: an async copy into a pinned buffer
         allocated once, then a wait on this object's stream (a pageable .cpu()
@@ -461,9 +468,7 @@ class SPBase:
         k = t.numel()
         if self.device.type != "cuda" or k > 64:
             return t.cpu().numpy()
-        pin = getattr(self, "_pin_small", None)
-        if pin is None:
-            pin = self._pin_small = torch.empty(64, dtype=torch.float64, pin_memory=True)
+        pin = self._pinned_small()
         stream = torch.cuda.current_stream(self.device)
         pin[:k].copy_(t.reshape(-1), non_blocking=True)
         stream.synchronize()

@@ -192,6 +192,8 @@ class SPOpt(SPBase):
         self.solve_stats.append(rec)
         if total.value == -1:
             self._solve_pending = True
+            if getattr(self, "_expect_ahead_wanted", False):
+                self._expect_ahead()
         else:
             self._record_solve(rec, int(total.value), 0)
         if self.extensions is not None:
@@ -296,10 +298,41 @@ class SPOpt(SPBase):
                                            self._stream()), "objective")
         self._bump()
 
+    def _expect_ahead(self):
+        """Iter0 (one rank): the expectations of the deferred solve's outputs
+        enqueued right behind it, with their copy into a pinned buffer, so that
+        E1 / feas_prob / Ebound read them with the solve's own wait instead of
+        a second device round trip.  Valid only if finishing the solve changes
+        no output (no scenario needed the generic path: the host epoch is
+        unchanged); _expect_sums checks that and recomputes otherwise."""
+        self._expect_ahead_state = None
+        if self.n_proc != 1 or self.device.type != "cuda":
+            return
+        lib = self._native
+        lib.check(self._ctx, lib.expect(self._ctx, self._prob.data_ptr(), self._outer.data_ptr(),
+                                        self._status.data_ptr(), self._expect_buf.data_ptr(),
+                                        self._stream()), "expect")
+        pin = self._pinned_small()
+        pin[:3].copy_(self._expect_buf[:3], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._expect_ahead_state = (self._host_epoch, ev)
+
     def _expect_sums(self):
         """[sum p*outer, sum p, sum p*[optimal]] over ALL ranks, on the host:
         one all-reduce and one device->host copy per solve (Iter0's E1,
         feas_prob and Ebound read the same three numbers)."""
+        ahead = getattr(self, "_expect_ahead_state", None)
+        if ahead is not None:
+            self._expect_ahead_state = None
+            self._settle()
+            epoch, ev = ahead
+            if epoch == self._host_epoch:
+                ev.synchronize()
+                self._expect_key = (self._outer.data_ptr(), self._host_epoch)   # _expect_buf holds them
+                self._expect_sums_val = self._pinned_small()[:3].numpy().copy()
+                self._expect_sums_key = self._expect_key
+                return self._expect_sums_val
         buf = self._expect(self._outer)
         key = self._expect_key
         if getattr(self, "_expect_sums_key", None) != key:

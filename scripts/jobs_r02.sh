@@ -34,5 +34,6 @@ case "$1" in
   s20) $J "bench:r02_s20_bench:--configs none --no-cpu-baseline --no-conv" "pmc:r02_s20_pmc_sq:$SQ:$B" \
           "bench:r02_s20_1m:$M" "pmc:r02_s20_pmc1m_fetch:FETCH_SIZE:$M" "pmc:r02_s20_pmc1m_write:WRITE_SIZE:$M" \
           "pmc:r02_s20_c5a_fetch:FETCH_SIZE:--only C5a $A" "pmc:r02_s20_c5a_write:WRITE_SIZE:--only C5a $A" ;;
+  s21) $J "test:tests" "bench:r02_s21_bench:--configs none --no-cpu-baseline --no-conv" "py:r02_s21_wall:scripts/iter0_wall.py" ;;
   *) echo "usage: $0 s8|s9|...|s20"; exit 2 ;;
 esac
