@@ -36,5 +36,7 @@ case "$1" in
           "pmc:r02_s20_c5a_fetch:FETCH_SIZE:--only C5a $A" "pmc:r02_s20_c5a_write:WRITE_SIZE:--only C5a $A" ;;
   s21) $J "test:tests" "bench:r02_s21_bench:--configs none --no-cpu-baseline --no-conv" "py:r02_s21_wall:scripts/iter0_wall.py" ;;
   s22) $J "py:r02_s22_smoke:scripts/run_smoke.py" "bench:r02_s22_bench:" ;;
+  s23) $J "test:tests/test_gpu_parity.py" "bench:r02_s23_bench:--configs none --no-cpu-baseline --no-conv" \
+          "bench:r02_s23_bench_b:--configs none --no-cpu-baseline --no-conv" ;;
   *) echo "usage: $0 s8|s9|...|s20"; exit 2 ;;
 esac
