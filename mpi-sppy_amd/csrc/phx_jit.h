@@ -217,16 +217,15 @@ inline std::string lane_kernel_source(const LaneStructure& L, int warm_waves = 1
          "  phx_lane::lane_stamp(io, 1);\n"
          "  const int t = blockIdx.x * 64 + threadIdx.x;\n"
          "  bool still = false;\n"
-         "  double dl = 0.0;\n"
          "  if (t < io.S) {\n"
-         "    if (io.fz.on) dl = phx_lane::fz_update_w<PT>(io, t);\n"
+         "    if (io.fz.on) (void)phx_lane::fz_update_w<PT>(io, t);\n"
          "    phx_lane::lane_stamp(io, 2);\n"
          "    still = " + wl + "(io, t);\n"
          "  }\n"
          "  phx_lane::lane_stamp(io, 3);\n"
          "  phx_lane::compact_lane(still, t, io.lanes_out, io.count_out);\n"
          "  phx_lane::lane_stamp(io, 4);\n"
-         "  if (io.fz.on) phx_lane::fz_epilogue<PT>(io, t, still, dl);\n"
+         "  if (io.fz.on) phx_lane::fz_epilogue<PT>(io, t, still);\n"
          "  phx_lane::lane_stamp(io, 5);\n"
          "}\n";
     // phx_iterk fused mode, after the last enqueued iteration: the decision on

@@ -762,7 +762,10 @@ PHX_LD void aset_store(const LaneIO& io, int sc, const ASet<PT>& a) {
         const uint32_t v = a.R(i) ? (a.lo(i) ? 1u : 2u) : 0u;
         w[b >> 5] |= v << (b & 31);
     }
-    PHX_UNROLL for (int k = 0; k < aset_words(PT::n(), PT::m()); ++k) io.aset[(int64_t)k * io.S + sc] = w[k];
+    // (the word addresses recomputed from an opaque index: kept from aset_load
+    // across the solve they were spilled to scratch)
+    const int so = opaque_index(sc);
+    PHX_UNROLL for (int k = 0; k < aset_words(PT::n(), PT::m()); ++k) io.aset[(int64_t)k * io.S + so] = w[k];
 }
 
 // Classify at an interior-point (x, y): a bound/row is active when its slack
@@ -1443,8 +1446,11 @@ __device__ double fz_update_w(const LaneIO& io, int sc) {
 // XCD the block ran on), the last shard's folder folds the shards and writes
 // the stage buffer of iteration k+1 (+ the straggler count of solve k and
 // this rank's conv sum).  Fixed order: independent of arrival order.
+// (the lane's sum |x_{k-1} - x-bar_k| is recomputed here from memory, the same
+// operations in the same order as fz_update_w: carried across the solve it was
+// one of the values spilled to scratch)
 template <class PT>
-__device__ void fz_epilogue(const LaneIO& io, int sc, bool still, double dl) {
+__device__ void fz_epilogue(const LaneIO& io, int sc, bool still) {
     const FusedW& f = io.fz;
     constexpr int NS = PT::nslot() > 0 ? PT::nslot() : 1;
     constexpr int NV = 2 * NS + 1;
@@ -1452,6 +1458,14 @@ __device__ void fz_epilogue(const LaneIO& io, int sc, bool still, double dl) {
     double v[NV];
     PHX_UNROLL for (int e = 0; e < NV; ++e) v[e] = 0.0;
     if (sc < io.S) {
+        double dl = 0.0;
+        PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
+            const int t = PT::col_slot(j);
+            if (t >= 0) {
+                const int64_t o = (int64_t)t * S + sc;
+                dl += fabs(f.x_prev[(int64_t)j * S + sc] - f.stage[io.xbar_idx[o]]);
+            }
+        }
         v[2 * NS] = dl;
         if (!still)
             PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {

@@ -38,5 +38,7 @@ case "$1" in
   s22) $J "py:r02_s22_smoke:scripts/run_smoke.py" "bench:r02_s22_bench:" ;;
   s23) $J "test:tests/test_gpu_parity.py" "bench:r02_s23_bench:--configs none --no-cpu-baseline --no-conv" \
           "bench:r02_s23_bench_b:--configs none --no-cpu-baseline --no-conv" ;;
+  s24) $J "test:tests" "bench:r02_s24_bench:--configs none --no-cpu-baseline --no-conv" \
+          "prof:r02_s24_prof:$B" "pmc:r02_s24_pmc_fetch:FETCH_SIZE:$B" "pmc:r02_s24_pmc_write:WRITE_SIZE:$B" ;;
   *) echo "usage: $0 s8|s9|...|s20"; exit 2 ;;
 esac
