@@ -40,5 +40,6 @@ case "$1" in
           "bench:r02_s23_bench_b:--configs none --no-cpu-baseline --no-conv" ;;
   s24) $J "test:tests" "bench:r02_s24_bench:--configs none --no-cpu-baseline --no-conv" \
           "prof:r02_s24_prof:$B" "pmc:r02_s24_pmc_fetch:FETCH_SIZE:$B" "pmc:r02_s24_pmc_write:WRITE_SIZE:$B" ;;
+  s25) $J "bench:r02_s25_1m:$M" "pmc:r02_s25_pmc1m_fetch:FETCH_SIZE:$M" "pmc:r02_s25_pmc1m_write:WRITE_SIZE:$M" ;;
   *) echo "usage: $0 s8|s9|...|s20"; exit 2 ;;
 esac
