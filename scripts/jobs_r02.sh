@@ -41,5 +41,6 @@ case "$1" in
   s24) $J "test:tests" "bench:r02_s24_bench:--configs none --no-cpu-baseline --no-conv" \
           "prof:r02_s24_prof:$B" "pmc:r02_s24_pmc_fetch:FETCH_SIZE:$B" "pmc:r02_s24_pmc_write:WRITE_SIZE:$B" ;;
   s25) $J "bench:r02_s25_1m:$M" "pmc:r02_s25_pmc1m_fetch:FETCH_SIZE:$M" "pmc:r02_s25_pmc1m_write:WRITE_SIZE:$M" ;;
+  s26) $J "prof:r02_s26_c2_prof:--only C2 $A" "prof:r02_s26_c5a_prof:--only C5a $A" "prof:r02_s26_c5b_prof:--only C5b $A" ;;
   *) echo "usage: $0 s8|s9|...|s20"; exit 2 ;;
 esac
