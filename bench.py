@@ -10,6 +10,13 @@ it fits one MI355X), rho = 1, scenarios sharded contiguously over the ranks
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
 
+With --gpus N > 1 and no WORLD_SIZE in the environment, this process launches
+the N ranks itself (torch.distributed.run, one process per GPU, 127.0.0.1
+rendezvous) before it makes any GPU call, and exits with their exit code -- the
+reference launches its ranks the same way (mpiexec -n N, examples/run_all.py:58-75).
+--device cpu (test hook): gloo + the test-only host emulation of the C ABI
+(tests/emu), no GPU call at all -- the launcher and the N-rank path run on CPU.
+
 Metric: value = S (K + 1) / T, T = wall time of Iter0 + K PH
 iterations (PHBase.Iter0 then PHBase.iterk_loop with PHIterLimit = K, on the
 device: phx_iterk), bracketed by barrier + device synchronize (none in between:
@@ -70,7 +77,55 @@ def parse():
     ap.add_argument("--configs", default="all", help="'all', 'none' or a comma list of C2,C4,C5a,C5b")
     ap.add_argument("--config-steps", type=int, default=10, help="K' of the other configs")
     ap.add_argument("--only", default=None, help="run one config as the headline (C2, C4, C5a, C5b)")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu: test hook (gloo + the host emulation library, no GPU)")
+    ap.add_argument("--ar-probe", type=int, default=1,
+                    help="N = 1: time phx_iterk with a no-op all-reduce callback (the per-iteration host "
+                         "cost of the Python collective hook)")
     return ap.parse_args()
+
+
+# ---------------------------------------------------------------- device plumbing
+class Dev:
+    """cuda: the GPU (RCCL for N > 1); cpu: the test hook (gloo, host emulation)."""
+
+    def __init__(self, kind):
+        self.kind = kind
+        self.cuda = kind == "cuda"
+        self.lib = None
+        self.device = None
+        if not self.cuda:
+            from mpisppy_amd import _native
+            self.lib = _native.Lib(os.path.join(_ROOT, "tests", "emu", "libphx_emu.so"), prefix="emu_phx_")
+            self.device = "cpu"
+
+    def sync(self):
+        if self.cuda:
+            torch.cuda.synchronize()
+
+    def tensor(self, vals):
+        return torch.tensor(vals, dtype=torch.float64, device="cuda" if self.cuda else "cpu")
+
+    def empty_cache(self):
+        if self.cuda:
+            torch.cuda.empty_cache()
+
+
+def launch_ranks(args):
+    """--gpus N > 1 without WORLD_SIZE: start N ranks (one process per GPU) as
+    children and return their exit code.  No GPU call happens in this process
+    (importing torch does not initialise the GPU)."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % args.gpus,
+           "--master-addr=127.0.0.1", "--master-port=%d" % port, os.path.abspath(__file__)] + sys.argv[1:]
+    print("[bench] launching %d ranks: %s" % (args.gpus, " ".join(cmd)), file=sys.stderr, flush=True)
+    return subprocess.run(cmd, env=env).returncode
 
 
 # ---------------------------------------------------------------- algorithmic bytes
@@ -201,39 +256,89 @@ def workloads():
     }
 
 
-def make_ph(w, S, cm, rho, so, iters, convthresh=1e-10):
+def make_ph(w, S, cm, rho, so, iters, dev, convthresh=1e-10, cls=None):
     from mpisppy_amd.opt.ph import PH
     opts = {"solver_name": "phx", "PHIterLimit": iters, "defaultPHrho": rho, "convthresh": convthresh,
             "verbose": False, "display_progress": False, "iter0_solver_options": dict(so),
             "iterk_solver_options": dict(so)}
-    return PH(opts, w["names"](S), w["creator"], scenario_creator_kwargs=w["kw"](S, cm), all_nodenames=w["nodes"])
+    return (cls or PH)(opts, w["names"](S), w["creator"], scenario_creator_kwargs=w["kw"](S, cm),
+                       all_nodenames=w["nodes"], _native_lib=dev.lib, _device=dev.device)
 
 
-def timed_run(ph, K):
+def timed_run(ph, K, dev):
     """Iter0 + K PH iterations, bracketed by barrier + synchronize (PH.ph_main without
     post_loops).  Returns (T, T_iter0, T_iterk), the max over ranks."""
     ph.PH_Prep()
     ph.subproblem_creation(False)
     ph.options["PHIterLimit"] = K
     ph.mpicomm.Barrier()
-    torch.cuda.synchronize()
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    dev.sync()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)] if dev.cuda else None
     t0 = time.perf_counter()
-    ev[0].record()
+    if ev:
+        ev[0].record()
     ph.Iter0()
     # (no synchronize between Iter0 and iterk_loop -- ph_main has none: the
     # Iter0 share is the device time between two events on the same stream,
     # its last work included)
-    ev[1].record()
+    if ev:
+        ev[1].record()
+    else:
+        t1 = time.perf_counter()
     ph.iterk_loop()
     ph._settle()
-    torch.cuda.synchronize()
+    dev.sync()
     ph.mpicomm.Barrier()
     t2 = time.perf_counter()
-    t1 = t0 + ev[0].elapsed_time(ev[1]) / 1e3
-    tt = torch.tensor([t2 - t0, t1 - t0, t2 - t1], dtype=torch.float64, device="cuda")
+    if ev:
+        t1 = t0 + ev[0].elapsed_time(ev[1]) / 1e3
+    tt = dev.tensor([t2 - t0, t1 - t0, t2 - t1])
     ph.mpicomm.allreduce_max_(tt)
     return [float(v) for v in tt.cpu()]
+
+
+def final_state(ph):
+    """The run's x-bar / conv (rank-independent: all-reduced), for checks of the N-rank path."""
+    xb = ph.xbar_by_node()
+    return {"xbar": {nd: [float(v) for v in a[0]] for nd, a in list(xb.items())[:4]}, "conv": ph.conv,
+            "trivial_bound": ph.trivial_bound}
+
+
+def ar_probe(w, S, cm, rho, so, K, dev):
+    """Host cost of the Python all-reduce hook of phx_iterk: the same K iterations
+    on one rank with and without a no-op callback installed (the multi-rank path
+    of phx_iterk: one or two callbacks per iteration, enqueued ahead of the GPU).
+    Returns the steady per-iteration times and the callback's own host time."""
+    from mpisppy_amd import _native
+    from mpisppy_amd.opt.ph import PH
+    calls = [0, 0.0]
+
+    class NoopPH(PH):
+        def _iterk_argstruct(self):
+            a = super()._iterk_argstruct()
+            if not getattr(self, "_noop_cb", None):
+                def cb(user, ptr, count, stream):
+                    t = time.perf_counter()
+                    calls[0] += 1
+                    calls[1] += time.perf_counter() - t
+                    return 0
+                self._noop_cb = _native.ALLREDUCE_FN(cb)
+                a.allreduce = self._noop_cb
+            return a
+
+    out = {}
+    for name, cls in (("without", PH), ("noop_callback", NoopPH)):
+        ph = make_ph(w, S, cm, rho, so, K, dev, cls=cls)
+        T, T0, Tk = timed_run(ph, K, dev)
+        out[name] = {"ms_per_iter": Tk * 1e3 / K, "fused": bool(getattr(ph, "iterk_stats", {}).get("fused"))}
+        del ph
+        dev.empty_cache()
+    out["callbacks"] = calls[0]
+    out["callbacks_per_iter"] = calls[0] / K
+    out["delta_us_per_iter"] = (out["noop_callback"]["ms_per_iter"] - out["without"]["ms_per_iter"]) * 1e3
+    out["note"] = ("a no-op ctypes callback on one rank (the N > 1 kernel path: conv test after the "
+                   "all-reduce); the real collective adds RCCL's own enqueue + latency")
+    return out
 
 
 def dominant_kernel(ph, K, fused):
@@ -277,15 +382,15 @@ def roofline(kernel, avg_s, launches, bpu, units, traffic=None, traffic_src=None
             "avg_launch_us": avg_s * 1e6, "launches": launches}
 
 
-def run_config(name, w, args, K, so, world):
+def run_config(name, w, args, K, so, world, dev):
     """One secondary config at N = 1: Iter0 + K iterations on a fresh PH object."""
     S = w["S"]
     so = dict(so, **w.get("so", {}))
     t = time.perf_counter()
-    ph = make_ph(w, S, 1, args.rho, so, K)
-    torch.cuda.synchronize()
+    ph = make_ph(w, S, 1, args.rho, so, K, dev)
+    dev.sync()
     setup = time.perf_counter() - t
-    T, T0, Tk = timed_run(ph, K)
+    T, T0, Tk = timed_run(ph, K, dev)
     kernel, avg_s, launches, bpu, units = dominant_kernel(ph, K, True)
     nbad = sum(s.get("not_optimal", 0) for s in ph.solve_stats)
     st = getattr(ph, "iterk_stats", None)
@@ -305,22 +410,29 @@ def run_config(name, w, args, K, so, world):
         res["cpu_baseline"] = cpu_baseline(args, model=c["model"], cm=c.get("cm", 1), scens=c["scens"],
                                            iters=c["iters"], total=c["total"])
     del ph
-    torch.cuda.empty_cache()
+    dev.empty_cache()
     return res
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print("[bench] --gpus %d but WORLD_SIZE=%d: running %d ranks" % (args.gpus, world, world),
+              file=sys.stderr, flush=True)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group(backend="nccl")
-    else:
+        if args.device == "cuda":
+            torch.cuda.set_device(local_rank)
+        dist.init_process_group(backend="nccl" if args.device == "cuda" else "gloo")
+    elif args.device == "cuda":
         torch.cuda.set_device(0)
     import mpisppy_amd  # noqa: F401
+    dev = Dev(args.device)
     W = workloads()
     K = args.steps
     so = {"lane_solver": args.lane_solver, "iterk_depth": args.depth, "iterk_timing": args.timing_every,
@@ -331,19 +443,19 @@ def main():
     cm = args.cm if args.only is None else 1
     # ---- warmup: a full untimed Iter0 + W iterations on its own object ----
     t = time.perf_counter()
-    ph = make_ph(hl, S, cm, args.rho, so, args.warmup)
+    ph = make_ph(hl, S, cm, args.rho, so, args.warmup, dev)
     print("[bench] warmup object built (%.1f s)" % (time.perf_counter() - t), file=sys.stderr, flush=True)
     ph.ph_main(finalize=False)
-    torch.cuda.synchronize()
+    dev.sync()
     t_warm = time.perf_counter() - t
     print("[bench] warmup done (%.1f s)" % t_warm, file=sys.stderr, flush=True)
     del ph
     # ---- timed: Iter0 + K iterations on a fresh object ----
     t = time.perf_counter()
-    ph = make_ph(hl, S, cm, args.rho, so, K)
-    torch.cuda.synchronize()
+    ph = make_ph(hl, S, cm, args.rho, so, K, dev)
+    dev.sync()
     t_setup = time.perf_counter() - t
-    T, T0, Tk = timed_run(ph, K)
+    T, T0, Tk = timed_run(ph, K, dev)
     print("[bench] timed run done (%.3f ms)" % (T * 1e3), file=sys.stderr, flush=True)
     st = getattr(ph, "iterk_stats", None)
     if st is not None and (st["iters"] != K or st["solves"] != K):
@@ -384,23 +496,29 @@ def main():
                  % (args.depth, ", fused" if st and st.get("fused") else "")) if st else "PHBase host loop",
         "not_optimal": nbad, "setup_s": t_setup, "warmup_s": t_warm,
         "solver": ph._native.jit_info(ph._ctx).decode(),
+        "final": final_state(ph),
     }
+    if args.device == "cpu":
+        res["device"] = "cpu (test hook: gloo + host emulation library; not a measurement)"
     del ph
-    torch.cuda.empty_cache()
+    dev.empty_cache()
     # ---- time to conv < 1e-4 from Iter0 (fresh object, same data) ----
     if not args.no_conv:
-        ph2 = make_ph(hl, S, cm, args.rho, so, args.conv_max_iters, convthresh=1e-4)
-        torch.cuda.synchronize()
+        ph2 = make_ph(hl, S, cm, args.rho, so, args.conv_max_iters, dev, convthresh=1e-4)
+        dev.sync()
         ph2.mpicomm.Barrier()
         t0 = time.perf_counter()
         ph2.ph_main(finalize=False)
-        torch.cuda.synchronize()
-        tc = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
+        dev.sync()
+        tc = dev.tensor([time.perf_counter() - t0])
         ph2.mpicomm.allreduce_max_(tc)
         res["conv_time"] = {"seconds": float(tc.item()), "iterations": ph2._PHIter, "conv": ph2.conv,
                             "convthresh": 1e-4, "converged": bool(ph2.conv is not None and ph2.conv < 1e-4)}
         del ph2
-        torch.cuda.empty_cache()
+        dev.empty_cache()
+    # ---- host cost of the Python all-reduce hook (one rank) ----
+    if world == 1 and args.only is None and args.ar_probe:
+        res["allreduce_hook"] = ar_probe(hl, S, cm, args.rho, so, K, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.only is None:
         res["cpu_baseline"] = cpu_baseline(args, cm=cm)
     # ---- the other BASELINE configs (one GPU) ----
@@ -409,7 +527,7 @@ def main():
         res["configs"] = {}
         for nm in names:
             try:
-                res["configs"][nm] = run_config(nm, W[nm], args, min(K, args.config_steps), so, world)
+                res["configs"][nm] = run_config(nm, W[nm], args, min(K, args.config_steps), so, world, dev)
             except Exception as e:     # reported, never hidden
                 res["configs"][nm] = {"error": repr(e)[:500]}
             print("[bench] %s done" % nm, file=sys.stderr, flush=True)

@@ -326,3 +326,79 @@ def netdes(sname, instance="network-10-10-H-01", num_scens=None):
     prob = 1.0 / num_scens if num_scens is not None else (float(z["p"][k]) if k < K else None)
     return Scen(sname, names, np.concatenate([z["c"], d]), 0.0, A, bl, bu, lb, ub,
                 [("ROOT", 1.0, 1, list(range(E)))], prob)
+
+
+# ---------------------------------------------------------------- hydro
+_HYDRO_JSON = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "mpi-sppy_amd", "examples",
+                           "data", "hydro.json")
+
+
+def hydro(sname, branching_factors=(3, 3)):
+    """hydro / elec3 three-stage LP (``mpisppy/tests/examples/hydro/hydro.py:31-236``),
+    written directly as a dense LP.  Columns: Pgt[1..3], Pgh[1..3], PDns[1..3],
+    Vol[1..3], sl, StageCost[1..3].  Rows: StageCost[t] - r_t (bGt Pgt + bGh Pgh +
+    bDns PDns) (- sl at t = 3) == 0; Pgt + Pgh + PDns == D[t]; Vol[t] - Vol[t-1] +
+    u[t] Pgh[t] <= u[t] A[t] (Vol[0] = V0 on the right); sl + 4166.67 Vol[3] >=
+    4166.67 V0.  r_t = (1/1.1)^(duracion[t]/T).  Nodes: ROOT [Pgt1, Pgh1, PDns1, Vol1],
+    ROOT_<(snum-1)//bf0> (cond_prob 1/bf0) the same of stage 2; uniform probability."""
+    import json
+    p = json.load(open(_HYDRO_JSON))["scenarios"][sname]
+    T = 3
+    col = {}
+    names = []
+    for fam in ["Pgt", "Pgh", "PDns", "Vol"]:
+        for t in range(1, T + 1):
+            col[fam, t] = len(names)
+            names.append("%s[%d]" % (fam, t))
+    col["sl"] = len(names)
+    names.append("sl")
+    for t in range(1, T + 1):
+        col["StageCost", t] = len(names)
+        names.append("StageCost[%d]" % t)
+    n = len(names)
+    lb, ub = np.zeros(n), np.zeros(n)
+    c = np.zeros(n)
+    for t in range(1, T + 1):
+        lb[col["Pgt", t]], ub[col["Pgt", t]] = p["PgtMin"], p["PgtMax"]
+        lb[col["Pgh", t]], ub[col["Pgh", t]] = p["PghMin"], p["PghMax"]
+        lb[col["PDns", t]], ub[col["PDns", t]] = 0.0, p["D"][str(t)]
+        lb[col["Vol", t]], ub[col["Vol", t]] = p["VMin"], p["VMax"]
+        lb[col["StageCost", t]], ub[col["StageCost", t]] = -INF, INF
+        c[col["StageCost", t]] = 1.0
+    lb[col["sl"]], ub[col["sl"]] = 0.0, INF
+    rows, bl, bu = [], [], []
+    for t in range(1, T + 1):
+        r_t = (1.0 / 1.1) ** (p["duracion"][str(t)] / p["T"])
+        a = np.zeros(n)
+        a[col["StageCost", t]] = 1.0
+        a[col["Pgt", t]] = -r_t * p["betaGt"]
+        a[col["Pgh", t]] = -r_t * p["betaGh"]
+        a[col["PDns", t]] = -r_t * p["betaDns"]
+        if t == T:
+            a[col["sl"]] = -1.0
+        rows.append(a); bl.append(0.0); bu.append(0.0)
+    for t in range(1, T + 1):
+        a = np.zeros(n)
+        a[col["Pgt", t]] = a[col["Pgh", t]] = a[col["PDns", t]] = 1.0
+        rows.append(a); bl.append(p["D"][str(t)]); bu.append(p["D"][str(t)])
+    for t in range(1, T + 1):
+        a = np.zeros(n)
+        u = p["u"][str(t)]
+        a[col["Vol", t]] = 1.0
+        a[col["Pgh", t]] = u
+        rhs = u * p["A"][str(t)]
+        if t == 1:
+            rhs += p["V0"]
+        else:
+            a[col["Vol", t - 1]] = -1.0
+        rows.append(a); bl.append(-INF); bu.append(rhs)
+    a = np.zeros(n)
+    a[col["sl"]] = 1.0
+    a[col["Vol", T]] = 4166.67
+    rows.append(a); bl.append(4166.67 * p["V0"]); bu.append(INF)
+    snum = extract_num(sname)
+    bf0 = branching_factors[0]
+    nodes = [("ROOT", 1.0, 1, [col["Pgt", 1], col["Pgh", 1], col["PDns", 1], col["Vol", 1]]),
+             ("ROOT_%d" % ((snum - 1) // bf0), 1.0 / bf0, 2,
+              [col["Pgt", 2], col["Pgh", 2], col["PDns", 2], col["Vol", 2]])]
+    return Scen(sname, names, c, 0.0, np.array(rows), bl, bu, lb, ub, nodes, None)

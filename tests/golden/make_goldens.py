@@ -55,6 +55,14 @@ def main():
                   "xhat [200,0] at every non-leaf node; 2 sig, 'rebaselined feb 2022')",
         "branching_factors": [4, 3, 2], "xhat_node": [200.0, 0.0],
         "evaluate": 1000.0, "evaluate_one_scen0": 1100.0, "sig": 2}
+    g["hydro_ph_bf33"] = {
+        "source": "mpisppy/tests/test_ef_ph.py:32-52 (options: rho 1, PHIterLimit 10, convthresh 0.001), "
+                  ":545-563 (BF [3,3], Scen1..Scen9, create_nodenames_from_branching_factors), "
+                  ":622-640 test_ph_solve (trivial bound 180, Eobjective after disable_W_and_prox 190; 2 sig), "
+                  ":581-601 test_ef_solve (EF Scen7.Pgt[2] 60; 1 sig)",
+        "branching_factors": [3, 3], "rho": 1.0, "PHIterLimit": 10, "convthresh": 0.001,
+        "trivial_bound": 180, "Eobj_W_prox_disabled": 190, "sig": 2,
+        "ef_Scen7_Pgt2": 60, "ef_sig": 1}
     with open(os.path.join(HERE, "ref_goldens.json"), "w") as f:
         json.dump(g, f, indent=1)
 

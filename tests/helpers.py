@@ -35,7 +35,7 @@ REF_W = np.array([[-16.10425295139681, 70.84705093609978, -54.742797934166234],
                   [57.20850439734766, -160.42352505639107, 103.21502058443501]])
 
 
-def oracle_continue_from(ph_iter0, scens, iters, rho=1.0):
+def oracle_continue_from(ph_iter0, scens, iters, rho=1.0, convthresh=1e-10):
     """The oracle's PH iterations 1..iters started from the engine's Iter0 point
     (degenerate Iter0 LPs may have several optimal vertices; from iteration 1 on the
     prox term makes each subproblem's nonant optimum unique, so the trajectories must
@@ -45,7 +45,7 @@ def oracle_continue_from(ph_iter0, scens, iters, rho=1.0):
     for k in range(len(scens)):
         o.x[k] = x[:, k].copy()
     o.W_on = o.prox_on = 1
-    o.iterk(iters, 1e-10)
+    o.iterk(iters, convthresh)
     return o
 
 

@@ -7,7 +7,7 @@ import os
 import numpy as np
 import pytest
 
-from helpers import oracle_continue_from, REF_W, REF_XBAR, rel, run_engine
+from helpers import all_certified, oracle_continue_from, REF_W, REF_XBAR, rel, run_engine
 from mpisppy_amd.examples import aircond, farmer
 from mpisppy_amd.utils import sputils
 from oracle import models as om, ph as oph
@@ -295,3 +295,44 @@ def test_native_loop_workgroup_stragglers_emu(emu):
     """One workgroup round per solve: lanes left to PDHG + polish stop the
     device loop, which finishes them and resumes (same trajectory)."""
     check_native_vs_host_wg(emu, "cpu", solver={"wg_warm": 1})   # (the stop count: GPU test)
+
+
+def check_reductions_by_iteration(lib, device, S, fused, K=3, rho=1.0):
+    """Compute_Xbar / Update_W / convergence_diff at full size, recomputed on the host
+    from the engine's own x (phbase.py:27-107, 293-343): runs with PHIterLimit =
+    0..K are deterministic prefixes of one another, so run k-1's nonants and W are
+    the inputs of run k's last iteration; its x-bar / x-sq-bar (math.fsum of
+    prob_coeff * x), W = W_old + rho (x - x-bar) and conv must agree to 1e-12
+    relative.  At S = 100,000 this checks the multi-tile / sharded-arrival reductions
+    (k_xbar, k_update_w_seg; in fused mode the warm kernel's x-bar partials from
+    iteration 2 on) independently of the oracle."""
+    import math
+    so = {"iterk_fused": fused}
+    runs = []
+    for k in range(K + 1):
+        ph, conv, Eobj, tb = run_engine(farmer.scenario_creator, farmer.scenario_names_creator(S),
+                                        {"num_scens": S}, k, rho=rho, lib=lib, device=device,
+                                        options={"iter0_solver_options": so, "iterk_solver_options": so})
+        assert all_certified(ph)
+        xb, xsq = ph.xbar_by_node()["ROOT"]
+        runs.append(dict(xn=ph.nonant_values(), W=ph.W_array(), xb=xb, xsq=xsq, conv=ph.conv,
+                         pc=ph._prob_coeff.copy(), fused=getattr(ph, "iterk_stats", {}).get("fused")))
+        del ph
+    for k in range(1, K + 1):
+        prev, cur = runs[k - 1], runs[k]
+        x, pc = prev["xn"], cur["pc"]
+        N = x.shape[1]
+        xb = np.array([math.fsum(pc[j] * x[:, j]) for j in range(N)])
+        xsq = np.array([math.fsum(pc[j] * x[:, j] * x[:, j]) for j in range(N)])
+        W = prev["W"] + rho * (x - xb[None, :])
+        conv = math.fsum(np.abs(x - xb[None, :]).ravel()) / (S * N)
+        assert rel(cur["xb"], xb) < 1e-12, k
+        assert rel(cur["xsq"], xsq) < 1e-12, k
+        assert rel(cur["W"], W) < 1e-12, k
+        assert abs(cur["conv"] - conv) <= 1e-12 * max(1.0, conv), k
+    return runs
+
+
+@pytest.mark.parametrize("fused", [0, 1])
+def test_reductions_by_iteration_emu(emu, fused):
+    check_reductions_by_iteration(emu, "cpu", 3000, fused)

@@ -104,6 +104,22 @@ def test_farmer_100k_sampled_oracle(gpu_lib):
     assert 0.0 < conv < 1e4 and np.isfinite(Eobj) and np.isfinite(tb)
 
 
+@pytest.mark.parametrize("fused", [0, 1])
+def test_farmer_100k_reductions_recheck(gpu_lib, fused):
+    """Full size (100,000 scenarios: 391 x-bar tiles, 8 arrival shards): after each of
+    3 PH iterations, x-bar / x-sq-bar / W / conv equal a host recomputation from the
+    engine's own x (math.fsum) to 1e-12 -- unfused (k_xbar + k_update_w_seg) and fused
+    (the warm kernel's x-bar partials and last-block fold from iteration 2 on)."""
+    from test_engine_emu import check_reductions_by_iteration
+    runs = check_reductions_by_iteration(gpu_lib, None, 100000, fused)
+    assert all(bool(r["fused"]) == bool(fused) for r in runs[1:])
+
+
+def test_uncertified_counts_infeasible_gpu(gpu_lib):
+    from test_xhat_emu import check_uncertified_counts_infeasible
+    check_uncertified_counts_infeasible(gpu_lib, None)
+
+
 def test_deferred_solve_with_stragglers_matches_sync(gpu_lib):
     """Deferred solve + optimistic Compute_Xbar/Update_W; stragglers forced by
     starving the interior point: the redo path must reproduce the synchronous run."""

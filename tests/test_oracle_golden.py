@@ -122,3 +122,39 @@ def test_xhat_eval_aircond():
     assert feas.all()
     assert round_pos_sig(E, g["sig"]) == g["evaluate"]
     assert round_pos_sig(objs[0], g["sig"]) == g["evaluate_one_scen0"]
+
+
+def hydro_oracle_ph():
+    """Test_hydro.test_ph_solve (test_ef_ph.py:622-640): hydro BF [3,3], rho 1,
+    PHIterLimit 10, convthresh 0.001 (test_ef_ph.py:32-52).  The reference's only
+    multistage PH pin: conditional prob_coeff (1/9 at ROOT, 1/3 at ROOT_b) and
+    per-node x-bar."""
+    g = G["hydro_ph_bf33"]
+    names = ["Scen%d" % k for k in range(1, 10)]
+    o = ph.OraclePH([models.hydro(n, g["branching_factors"]) for n in names], rho=g["rho"])
+    conv, Eobj, tb = o.ph_main(g["PHIterLimit"], g["convthresh"])
+    o.W_on = o.prox_on = 0                       # ph.disable_W_and_prox()
+    return o, conv, Eobj, tb, o.Eobjective()
+
+
+def test_hydro_ph_pin():
+    g = G["hydro_ph_bf33"]
+    o, conv, Eobj, tb, E_noWprox = hydro_oracle_ph()
+    assert round_pos_sig(tb, g["sig"]) == g["trivial_bound"]
+    assert round_pos_sig(E_noWprox, g["sig"]) == g["Eobj_W_prox_disabled"]
+    # per-node x-bar: ROOT over all 9 scenarios, each ROOT_b over its 3 (p/uncond = 1/3)
+    xn = o.xn()
+    o.compute_xbar()
+    assert np.allclose(o.xbar[0, :4], xn[:, :4].mean(0), rtol=1e-12, atol=1e-12)
+    for b in range(3):
+        assert np.allclose(o.xbar[3 * b, 4:], xn[3 * b:3 * b + 3, 4:].mean(0), rtol=1e-12, atol=1e-12)
+
+
+def test_hydro_ef_pin():
+    """Test_hydro.test_ef_solve (test_ef_ph.py:581-601): Scen7.Pgt[2] of the EF ~ 60."""
+    g = G["hydro_ph_bf33"]
+    scens = [models.hydro("Scen%d" % k, g["branching_factors"]) for k in range(1, 10)]
+    obj, x, st = ph.solve_ef(scens)
+    n = len(scens[0].c)
+    j = scens[6].var_names.index("Pgt[2]")
+    assert round_pos_sig(x[6 * n + j], g["ef_sig"]) == g["ef_Scen7_Pgt2"]

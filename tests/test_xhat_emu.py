@@ -194,3 +194,25 @@ def test_fixed_in_pre_iter0_stay_fixed_in_post_solve_bound_emu(emu):
     o.W_on, o.prox_on = 1, 0
     o.solve_loop()
     assert rel(bound, o.Ebound()) < 1e-9
+
+
+def check_uncertified_counts_infeasible(lib, device):
+    """A lane the solver leaves uncertified (iteration limit: PDHG capped at one
+    chunk, no polish, no interior point) loads no certified solution, so it is
+    not feasible (spopt.py:175-207 sets scenario_feasible only for a loaded
+    solution): feas_prob drops and infeas_prob rises by its probability, and
+    calculate_incumbent returns None (xhat_eval.py:406-430)."""
+    so = {"lane_solver": 0, "polish": 0, "pdhg_max_iters": 64, "pdhg_check_every": 64, "ipm_after": -1,
+          "wg_warm": 0, "sp": 0}
+    ev = farmer_eval(lib, device, 6, 6, solver_options=so)
+    ev.current_solver_options = so
+    ev.evaluate({"ROOT": np.array([80.0, 250.0, 170.0])})
+    st = ev._status.cpu().numpy()
+    assert (st != 1).all(), st
+    assert ev.infeas_prob() == pytest.approx(1.0)
+    assert ev.feas_prob() == pytest.approx(0.0)
+    assert ev.calculate_incumbent() is None
+
+
+def test_uncertified_counts_infeasible_emu(emu):
+    check_uncertified_counts_infeasible(emu, "cpu")
