@@ -219,7 +219,7 @@ def cpu_baseline(args, model="farmer", cm=1, scens=None, iters=None, total=None,
     if r.returncode != 0:
         return {"error": r.stderr[-500:]}
     d = json.loads(r.stdout.strip().splitlines()[-1])
-    return {k: d[k] for k in ["value", "unit", "cores", "kind", "sample", "seconds"]}
+    return {k: d[k] for k in ["value", "unit", "cores", "kind", "sample", "seconds", "host"]}
 
 
 # ---------------------------------------------------------------- workloads
@@ -234,7 +234,7 @@ def workloads():
         "C2": dict(creator=farmer.scenario_creator, names=lambda S: farmer.scenario_names_creator(1000),
                    kw=lambda S, cm: {"num_scens": 1000, "crops_multiplier": 10}, nodes=None, S=1000,
                    desc="farmer crops_multiplier=10, 1,000 scenarios (BASELINE configs[1])",
-                   cpu=dict(model="farmer", cm=10, scens=256, iters=2, total=1000)),
+                   cpu=dict(model="farmer", cm=10, scens=1000, iters=2, total=1000)),
         "C4": dict(creator=aircond.scenario_creator, names=lambda S: ["scen%d" % i for i in range(1000)],
                    kw=lambda S, cm: {"branching_factors": bfs}, S=1000,
                    nodes=sputils.create_nodenames_from_branching_factors(bfs),
@@ -248,11 +248,11 @@ def workloads():
                     # (measured: 16 rounds 24.4, 8 18.9, 4 16.3 ms per iteration;
                     # profiles/r02_s18_wg_rounds.txt)
                     so={"wg_warm": 4},
-                    cpu=dict(model="sslp", scens=128, iters=1, total=10000)),
+                    cpu=dict(model="sslp", scens=512, iters=2, total=10000)),
         "C5b": dict(creator=netdes.scenario_creator, names=lambda S: netdes.scenario_names_creator(10000),
                     kw=lambda S, cm: {"instance": "network-50-30-H-01", "num_scens": 10000}, nodes=None, S=10000,
                     desc="netdes network-50-30-H LP relaxation, 10,000 scenarios (BASELINE configs[4])",
-                    cpu=dict(model="netdes50", scens=32, iters=1, total=10000)),
+                    cpu=dict(model="netdes50", scens=256, iters=4, total=10000)),
     }
 
 

@@ -50,9 +50,28 @@ def names_of(model, S):
     return ["Scenario%d" % i for i in range(S)]
 
 
+def fast_solver(scens):
+    """The baseline's per-subproblem solve: a persistent HiGHS instance per scenario
+    (costs and prox Hessian changed per solve, warm from its last basis: the
+    reference's persistent solver plugins) + one dense KKT polish of its basis
+    (qp.solve_fast; the iterated certified polish only when that point fails the
+    certificate) for small subproblems; the oracle's sparse path (qp.solve) for large
+    ones (sslp, netdes)."""
+    from oracle import qp
+    small = all(s.A.shape[0] + s.A.shape[1] <= 300 for s in scens)
+    if not small:
+        return qp.solve
+    inst = {id(s.A): qp.PersistentHighs(s.A, s.bl, s.bu, s.lb, s.ub) for s in scens}
+
+    def solve(A, bl, bu, lb, ub, q, p):
+        return qp.solve_fast(A, bl, bu, lb, ub, q, p, hs=inst.get(id(A)))
+    return solve
+
+
 def _worker(conn, names, S, cm, rho, model="farmer"):
     scens = [make_scen(model, nm, S, cm) for nm in names]
     o = oph.OraclePH(scens, rho=rho)
+    o.solver = fast_solver(scens)
     o.iter0()
     conn.send((o.xn(), o.obj.copy()))
     while True:
@@ -104,10 +123,26 @@ def run(S, K, P, cm=1, rho=1.0, model="farmer", S_total=None):
         p.join()
     return {"value": S * K / dt, "unit": "scenario-iterations/s", "cores": P, "kind": "port",
             "seconds": dt, "setup_and_iter0_seconds": t_setup, "conv_last": conv,
-            "sample": "oracle PH restatement (numpy + scipy-HiGHS 1.8 LP/QP or sparse IPM + certified KKT "
-                      "polish), %s, %d scenarios x %d PH iterations after Iter0, %d worker processes "
-                      "(contiguous slices, parent = Allreduce)"
-                      % ("farmer cm=%d" % cm if model == "farmer" else model, S, K, P)}
+            "sample": "oracle PH restatement (numpy + persistent scipy-HiGHS 1.8 LP/QP + one KKT polish of its basis; "
+                      "sparse IPM + certified polish above 300 rows+cols), %s, %d scenarios x %d PH iterations "
+                      "after Iter0, %d worker processes (contiguous slices, parent = Allreduce)"
+                      % ("farmer cm=%d" % cm if model == "farmer" else model, S, K, P),
+            "host": host_info()}
+
+
+def host_info():
+    """nproc and the CPU model of the machine the baseline ran on."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None
+    return {"nproc": os.cpu_count(), "affinity_cpus": aff, "cpu_model": model}
 
 
 def main():

@@ -97,9 +97,10 @@ class OraclePH:
         return f
 
     def solve_loop(self):
+        solve = getattr(self, "solver", None) or qp.solve
         for k, s in enumerate(self.scens):
             q, p = self._qp_data(k)
-            x, feas = qp.solve(s.A, s.bl, s.bu, s.lb, s.ub, q, p)
+            x, feas = solve(s.A, s.bl, s.bu, s.lb, s.ub, q, p)
             if not feas:
                 raise RuntimeError("oracle: infeasible scenario %s" % s.name)
             self.x[k] = x

@@ -388,3 +388,116 @@ def solve(A, bl, bu, lb, ub, q, p=None, do_polish=True):
     STATS["solves"] += 1
     STATS["rounds"] += rounds
     return xp, True
+
+
+def _certified(A, bl, bu, lb, ub, q, p, x, y, cc, rc, tol=1e-9):
+    """certified_polish's KKT certificate of (x, y) for the active set (cc, rc), dense."""
+    fin = lambda v: np.where(np.isfinite(v), v, 0.0)
+    ax = A @ x
+    z = p * x + q - A.T @ y
+    dtol = tol * (1.0 + np.max(np.abs(q))) if len(q) else tol
+    bad = ((lb - x) > tol * (1.0 + np.abs(fin(lb)))).any() or ((x - ub) > tol * (1.0 + np.abs(fin(ub)))).any()
+    bad = bad or ((bl - ax) > tol * (1.0 + np.abs(fin(bl)))).any() or ((ax - bu) > tol * (1.0 + np.abs(fin(bu)))).any()
+    fixed, eqr = lb == ub, bl == bu
+    bad = bad or ((cc == 1) & ~fixed & (z < -dtol)).any() or ((cc == 2) & ~fixed & (z > dtol)).any()
+    bad = bad or ((rc == 1) & ~eqr & (y < -dtol)).any() or ((rc == 2) & ~eqr & (y > dtol)).any()
+    bad = bad or ((cc == 0) & (np.abs(z) > dtol)).any()
+    return not bad
+
+
+class PersistentHighs:
+    """One HiGHS instance per subproblem, kept across PH iterations: each solve
+    changes only the costs and the (diagonal) prox Hessian and re-runs from the
+    previous basis -- the analogue of the reference's persistent solver plugins
+    (``spopt.py:129-142``: set_instance once, set_objective per solve)."""
+
+    def __init__(self, A, bl, bu, lb, ub):
+        Ac = as_csc(A)
+        m, n = Ac.shape
+        self.n = n
+        h = _core._Highs()
+        h.setOptionValue("output_flag", False)
+        h.setOptionValue("primal_feasibility_tolerance", 1e-10)
+        h.setOptionValue("dual_feasibility_tolerance", 1e-10)
+        h.setOptionValue("qp_iteration_limit", 20000)
+        h.setOptionValue("time_limit", 20.0)
+        lp = _core.HighsLp()
+        lp.num_col_, lp.num_row_ = n, m
+        lp.col_cost_ = np.zeros(n)
+        lp.col_lower_, lp.col_upper_ = _to_highs_bound(lb), _to_highs_bound(ub)
+        lp.row_lower_, lp.row_upper_ = _to_highs_bound(bl), _to_highs_bound(bu)
+        lp.a_matrix_.format_ = _core.MatrixFormat.kColwise
+        lp.a_matrix_.start_ = Ac.indptr.astype(np.int32)
+        lp.a_matrix_.index_ = Ac.indices.astype(np.int32)
+        lp.a_matrix_.value_ = Ac.data.astype(np.float64)
+        lp.a_matrix_.num_col_, lp.a_matrix_.num_row_ = n, m
+        h.passModel(lp)
+        self.h = h
+        self.cols = np.arange(n, dtype=np.int32)
+
+    def solve(self, q, p):
+        h, n = self.h, self.n
+        h.changeColsCost(n, self.cols, np.asarray(q, dtype=np.float64))
+        hs = _core.HighsHessian()
+        hs.dim_ = n
+        hs.format_ = _core.HessianFormat.kTriangular
+        nzc = np.nonzero(p)[0]
+        st = np.zeros(n + 1, dtype=np.int32)
+        st[1:] = np.cumsum(p != 0)
+        hs.start_, hs.index_, hs.value_ = st, nzc.astype(np.int32), p[nzc]
+        h.passHessian(hs)
+        h.run()
+        status = h.modelStatusToString(h.getModelStatus())
+        x = np.asarray(h.getSolution().col_value, dtype=np.float64)
+        cs = rs = None
+        b = h.getBasis()
+        if b.valid:
+            cs = np.array([int(v) for v in b.col_status])
+            rs = np.array([int(v) for v in b.row_status])
+        return x, status, cs, rs
+
+
+def solve_fast(A, bl, bu, lb, ub, q, p=None, hs=None):
+    """The CPU baseline's subproblem solve (oracle/cpu_bench.py): HiGHS (hs: the
+    subproblem's PersistentHighs), then ONE dense KKT polish of HiGHS's basis; the
+    iterated certified polish (solve) runs only when that point fails the same
+    certificate.  Dense A (small subproblems: farmer).  Returns (x, feasible)."""
+    n = A.shape[1]
+    q = np.asarray(q, dtype=np.float64)
+    p = np.zeros(n) if p is None else np.asarray(p, dtype=np.float64)
+    if hs is not None:
+        x0, status, cs, rs = hs.solve(q, p)
+    else:
+        x0, status, cs, rs = highs_solve(A, bl, bu, lb, ub, q, p, want_basis=True)
+    if status != "Optimal" or cs is None:
+        return solve(A, bl, bu, lb, ub, q, p)
+    cc, rc = _initial_active_set(A, bl, bu, lb, ub, x0, cs, rs)
+    F = np.nonzero(cc == 0)[0]
+    R = np.nonzero(rc != 0)[0]
+    x = x0.copy()
+    x[cc == 1] = lb[cc == 1]
+    x[cc == 2] = ub[cc == 2]
+    B = np.nonzero(cc != 0)[0]
+    A_RF = A[np.ix_(R, F)]
+    nF, nR = len(F), len(R)
+    K = np.zeros((nF + nR, nF + nR))
+    K[np.arange(nF), np.arange(nF)] = p[F]
+    K[:nF, nF:] = -A_RF.T
+    K[nF:, :nF] = A_RF
+    r = np.concatenate([-q[F], np.where(rc[R] == 1, bl[R], bu[R]) - A[np.ix_(R, B)] @ x[B]])
+    try:
+        s = np.linalg.solve(K, r) if nF + nR else np.zeros(0)
+    except np.linalg.LinAlgError:
+        s = None
+    if s is not None and np.all(np.isfinite(s)):
+        x[F] = s[:nF]
+        y = np.zeros(len(bl))
+        y[R] = s[nF:]
+        if _certified(A, bl, bu, lb, ub, q, p, x, y, cc, rc):
+            STATS["solves"] += 1
+            STATS["rounds"] += 1
+            return x, True
+    xp, _, rounds = certified_polish(A, bl, bu, lb, ub, q, p, x0, cs, rs)
+    STATS["solves"] += 1
+    STATS["rounds"] += rounds
+    return xp, True

@@ -1,0 +1,15 @@
+#!/bin/bash
+# Round-3 GPU evidence jobs (run through gpurun): bash scripts/jobs_r03.sh <name>.
+# Each job is a list of scripts/gpu_job.sh steps; logs land in gpurun_out/, the
+# summaries judged are copied into profiles/ (named after the job).
+set -o pipefail
+B="--configs none --no-cpu-baseline --no-conv --steps 50"                 # headline, K = 50
+H="--configs none --no-cpu-baseline --no-conv"                            # headline, K = 20 (driver shape)
+M="--configs none --no-cpu-baseline --no-conv --steps 20 --warmup 1 --scens 1000000 --ar-probe 0"   # over-cache 1M
+A="--no-cpu-baseline --no-conv --steps 10 --warmup 1"                     # one secondary config
+SQ="SQ_INSTS_VALU,SQ_ACTIVE_INST_VALU,SQ_WAVE_CYCLES,SQ_WAIT_ANY,SQ_INSTS_VALU_FLOPS_FP64,SQ_INSTS_SALU"
+J="bash scripts/gpu_job.sh"
+case "$1" in
+  s1)  $J "test:tests" "bench:r03_s1_bench:$H" ;;
+  *) echo "unknown job $1"; exit 2 ;;
+esac
