@@ -327,8 +327,12 @@ def ar_probe(w, S, cm, rho, so, K, dev):
             return a
 
     out = {}
-    for name, cls in (("without", PH), ("noop_callback", NoopPH)):
-        ph = make_ph(w, S, cm, rho, so, K, dev, cls=cls)
+    variants = [("without", PH, so), ("noop_callback", NoopPH, so)]
+    if dev.cuda:
+        # the N > 1 path with phx_iterk's own RCCL all-reduce (one-rank communicator)
+        variants.append(("rccl_in_loop_1rank", PH, dict(so, native_comm=2)))
+    for name, cls, sov in variants:
+        ph = make_ph(w, S, cm, rho, sov, K, dev, cls=cls)
         T, T0, Tk = timed_run(ph, K, dev)
         out[name] = {"ms_per_iter": Tk * 1e3 / K, "fused": bool(getattr(ph, "iterk_stats", {}).get("fused"))}
         del ph
@@ -336,8 +340,12 @@ def ar_probe(w, S, cm, rho, so, K, dev):
     out["callbacks"] = calls[0]
     out["callbacks_per_iter"] = calls[0] / K
     out["delta_us_per_iter"] = (out["noop_callback"]["ms_per_iter"] - out["without"]["ms_per_iter"]) * 1e3
+    if "rccl_in_loop_1rank" in out:
+        out["rccl_delta_us_per_iter"] = (out["rccl_in_loop_1rank"]["ms_per_iter"]
+                                         - out["without"]["ms_per_iter"]) * 1e3
     out["note"] = ("a no-op ctypes callback on one rank (the N > 1 kernel path: conv test after the "
-                   "all-reduce); the real collective adds RCCL's own enqueue + latency")
+                   "all-reduce) vs phx_iterk's own ncclAllReduce on a one-rank communicator (the default "
+                   "for N > 1 on GPUs); a real N-rank collective adds its xGMI latency")
     return out
 
 

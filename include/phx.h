@@ -333,6 +333,20 @@ typedef struct phx_iterk_result {
 int phx_iterk(phx_ctx* ctx, const phx_solve_opts* opts, const phx_iterk_args* args,
               phx_iterk_result* result_host, void* stream);
 
+/* The context's own collective for phx_iterk: an RCCL communicator over the
+ * ranks of the PH cylinder (one process per GPU), so the per-iteration
+ * all-reduce of the fused node buffer is enqueued by phx_iterk itself
+ * (ncclAllReduce, SUM, fp64, on the loop's stream) instead of a host callback.
+ * Replaces the per-tree-node comms[ndn].Allreduce of _Compute_Xbar
+ * (phbase.py:83-87) and the ROOT Allreduce of convergence_diff
+ * (phbase.py:341) inside the loop, and the Split communicators they run on
+ * (spbase.py:333-375).  phx_comm_unique_id: one rank draws the id (128 bytes,
+ * host) and the caller broadcasts it; phx_set_comm: collective over the
+ * nranks ranks (ncclCommInitRank).  phx_iterk uses the communicator when
+ * args.allreduce is NULL.                                                    */
+int phx_comm_unique_id(void* id_host);
+int phx_set_comm(phx_ctx* ctx, const void* id_host, int32_t nranks, int32_t rank);
+
 /* Everything phx_iterk allocates or uploads for these arguments (segment
  * tiles, control words, the mapped progress word, the fused mode's second
  * output set, timing events), done ahead of the loop; no work is enqueued.

@@ -97,7 +97,7 @@ class IterkResult(ctypes.Structure):
 SYMBOLS = [
     "create", "destroy", "last_error", "build_info", "set_problem", "set_bounds", "set_ph_terms",
     "solve", "solve_finish", "objective", "xbar", "update_w", "expect", "export_slots", "last_solve_stats", "jit_info",
-    "iterk", "iterk_prepare",
+    "iterk", "iterk_prepare", "comm_unique_id", "set_comm",
 ]
 
 
@@ -149,6 +149,8 @@ class Lib:
         self.iterk = fn("iterk", ctypes.c_int, [c_void_p, ctypes.POINTER(SolveOpts), ctypes.POINTER(IterkArgs),
                                                 ctypes.POINTER(IterkResult), c_void_p])
         self.iterk_prepare = fn("iterk_prepare", ctypes.c_int, [c_void_p, ctypes.POINTER(IterkArgs)])
+        self.comm_unique_id = fn("comm_unique_id", ctypes.c_int, [c_void_p])
+        self.set_comm = fn("set_comm", ctypes.c_int, [c_void_p, c_void_p, c_int32, c_int32])
 
     def check(self, ctx, rc, what):
         if rc != 0:

@@ -53,8 +53,11 @@ class PHBase(SPOpt):
         self.attach_xbars()
         # the device loop's buffers and events, allocated with the problem
         # (phx_iterk_prepare) so no PH iteration pays an allocation
+        self._native_comm = False
         if (self.batch.nonant.N > 0 and self.NNS > 0
                 and self._device_loop_solver(self._solve_opts(self.iterk_solver_options))):
+            if self._want_native_comm():
+                self._setup_native_comm()
             lib = self._native
             lib.check(self._ctx, lib.iterk_prepare(self._ctx, ctypes.byref(self._iterk_argstruct())),
                       "iterk_prepare")
@@ -402,6 +405,29 @@ class PHBase(SPOpt):
         return ("workgroup solver on" in info and int(so.wg_warm) > 0 and int(so.polish) > 0
                 and int(so.warm_start) > 0)
 
+    def _want_native_comm(self):
+        """phx_iterk's per-iteration all-reduce from C (an RCCL communicator of
+        the context, phx_set_comm) rather than a Python callback into
+        torch.distributed: on GPUs with several ranks over RCCL by default
+        (iterk_solver_options {"native_comm": 0} keeps the callback; 2 also
+        builds a one-rank communicator, a test hook for the RCCL path)."""
+        mode = int((self.iterk_solver_options or {}).get("native_comm", 1))
+        if self.device.type != "cuda" or mode == 0:
+            return False
+        return mode == 2 or (self.n_proc > 1 and self.mpicomm.backend == "nccl")
+
+    def _setup_native_comm(self):
+        """Collective over the cylinder's ranks: rank 0 draws an RCCL unique id,
+        the communicator broadcasts it, every rank joins (ncclCommInitRank)."""
+        lib = self._native
+        uid = ctypes.create_string_buffer(128)
+        if self.cylinder_rank == 0:
+            lib.check(self._ctx, lib.comm_unique_id(uid), "comm_unique_id")
+        raw = self.mpicomm.bcast(uid.raw if self.cylinder_rank == 0 else None, root=0)
+        uid = ctypes.create_string_buffer(raw, 128)
+        lib.check(self._ctx, lib.set_comm(self._ctx, uid, self.n_proc, self.cylinder_rank), "set_comm")
+        self._native_comm = True
+
     def _allreduce_cb(self):
         if getattr(self, "_ar_cb", None) is None:
             bufs = {self._node_stage.data_ptr(): self._node_stage, self._seg_sums.data_ptr(): self._seg_sums}
@@ -474,7 +500,7 @@ class PHBase(SPOpt):
             self._conv_counts_c = (ctypes.c_double * len(self._conv_counts))(*self._conv_counts)
             a.conv_counts_host = ctypes.cast(self._conv_counts_c, ctypes.c_void_p)
             a.conv_R = self._conv_R
-            if self.n_proc > 1:
+            if self.n_proc > 1 and not self._native_comm:
                 a.allreduce = self._allreduce_cb()
             a.depth = 4
             self._iterk_args = a

@@ -372,3 +372,24 @@ def test_native_loop_workgroup_stragglers_gpu(gpu_lib):
     from test_engine_emu import check_native_vs_host_wg
     a, b = check_native_vs_host_wg(gpu_lib, None, S=300, iters=5, solver={"wg_warm": 1})
     assert a.iterk_stats["straggler_stops"] > 0
+
+
+@pytest.mark.parametrize("fused", [0, 1])
+def test_native_rccl_path_one_rank_gpu(gpu_lib, fused):
+    """phx_iterk's own RCCL all-reduce (phx_set_comm + ncclAllReduce on the loop's
+    stream: the N > 1 path with the device-side conv test after the collective),
+    exercised on one rank through a one-rank communicator: the same trajectory
+    as the single-rank loop."""
+    S = 2000
+    res = []
+    for nc in (0, 2):
+        so = {"native_comm": nc, "iterk_fused": fused}
+        ph, conv, Eobj, tb = run_engine(farmer.scenario_creator, farmer.scenario_names_creator(S), {"num_scens": S},
+                                        6, lib=gpu_lib, options={"iter0_solver_options": so,
+                                                                 "iterk_solver_options": so})
+        assert ph._native_comm == bool(nc) and hasattr(ph, "iterk_stats")
+        assert bool(ph.iterk_stats["fused"]) == bool(fused)
+        res.append((ph.W_array(), ph.xbar_by_node()["ROOT"][0], conv, Eobj))
+    (W0, x0, c0, E0), (W1, x1, c1, E1) = res
+    assert rel(W1, W0) < 1e-12 and rel(x1, x0) < 1e-12
+    assert rel(c1, c0) < 1e-12 and rel(E1, E0) < 1e-12
