@@ -462,6 +462,7 @@ class PHBase(SPOpt):
         self._settle()
         self._apply_fixing()
         self._set_ph_terms()
+        self._x_touched = True
         lib = self._native
         so_dict = self.current_solver_options or {}
         so = self._solve_opts(so_dict)

@@ -375,6 +375,7 @@ class SPBase:
         self._desc = desc
         # PH state
         self._x = torch.zeros(n * S, dtype=f64, device=self.device)
+        self._x_touched = False          # x still all zeros (SPOpt._save_original_nonants)
         self._y = torch.zeros(max(m, 1) * S, dtype=f64, device=self.device)
         self._obj = torch.zeros(S, dtype=f64, device=self.device)
         self._iter0_obj_dev = torch.zeros(S, dtype=f64, device=self.device)   # Iter0's optima (PHBase)
@@ -443,6 +444,11 @@ class SPBase:
         self._seg_s1 = (_native.c_int32 * len(segs))(*[b for _, b in segs])
         self._host_epoch = 0
         self._host_cache = {}
+        # the stream handle and the small pinned buffer, looked up / allocated now
+        # rather than inside the first timed PH step
+        self._stream()
+        if self.device.type == "cuda":
+            self._pinned_small()
 
     def _stream(self):
         """The stream every native call is ordered on: the device's current
@@ -511,6 +517,8 @@ class SPBase:
         S = self._S
         if hasattr(self, "_settle"):
             self._settle()
+        if key == "x":
+            self._x_touched = True
         t = self._x if key == "x" else {"W": self._W, "rho": self._rho}[key]
         t[j * S + s] = float(value)
         if key in self._host_cache:

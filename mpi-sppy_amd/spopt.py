@@ -116,6 +116,19 @@ class SPOpt(SPBase):
 
     # ------------------------------------------------------------ solve
     def _solve_opts(self, solver_options):
+        """phx_solve_opts from a solver-options dict (cached per dict contents; a
+        fresh struct is returned, so callers may modify it)."""
+        key = tuple(sorted((k, v) for k, v in (solver_options or {}).items()
+                           if k in SOLVER_DEFAULTS and isinstance(v, (int, float))))
+        cache = self.__dict__.setdefault("_solve_opts_cache", {})
+        so = cache.get(key)
+        if so is None:
+            so = cache[key] = self._make_solve_opts(solver_options)
+        out = _native.SolveOpts()
+        ctypes.pointer(out)[0] = so
+        return out
+
+    def _make_solve_opts(self, solver_options):
         o = dict(SOLVER_DEFAULTS)
         if solver_options:
             for k, v in solver_options.items():
@@ -179,6 +192,7 @@ class SPOpt(SPBase):
         self._set_ph_terms()
         total = ctypes.c_int32(0)
         t0 = time.perf_counter()
+        self._x_touched = True
         lib.check(self._ctx, lib.solve(self._ctx, ctypes.byref(so), self._x.data_ptr(), self._y.data_ptr(),
                                        self._obj.data_ptr(), self._status.data_ptr(), self._iters.data_ptr(),
                                        ctypes.byref(total), self._stream()), "solve")
@@ -412,6 +426,7 @@ class SPOpt(SPBase):
     def _set_nonant_x(self, vals, mask=None):
         """Write nonant values (S_local, N) into x on the device (where mask)."""
         self._settle()
+        self._x_touched = True
         nn = self.batch.nonant
         S = self._S
         cols = torch.as_tensor(nn.slot_col.astype(np.int64), device=self.device)
@@ -517,7 +532,9 @@ class SPOpt(SPBase):
         copied only when something was ever fixed."""
         self._settle()
         S = self._S
-        torch.index_select(self._x.view(-1, S), 0, self._slot_cols_dev, out=self._orig_nonants_dev)
+        if getattr(self, "_x_touched", True):
+            torch.index_select(self._x.view(-1, S), 0, self._slot_cols_dev, out=self._orig_nonants_dev)
+        # (else x still holds its initial zeros, as _orig_nonants_dev does: nothing to copy)
         self._orig_nonants_saved = True
         self._orig_nonants_host = None
         fixed = getattr(self, "_fixed", None)
