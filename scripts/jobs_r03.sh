@@ -11,5 +11,6 @@ SQ="SQ_INSTS_VALU,SQ_ACTIVE_INST_VALU,SQ_WAVE_CYCLES,SQ_WAIT_ANY,SQ_INSTS_VALU_F
 J="bash scripts/gpu_job.sh"
 case "$1" in
   s1)  $J "test:tests" "bench:r03_s1_bench:$H" ;;
+  s2)  $J "trace:r03_s2_trace:$H --ar-probe 0" "prof:r03_s2_prof:$H --ar-probe 0" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
