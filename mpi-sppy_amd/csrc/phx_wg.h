@@ -46,6 +46,19 @@ struct WgPairs {
     const int32_t* ib;    // [npair]
     const int32_t* ka;    // [ntrip]
     const int32_t* kb;    // [ntrip]
+    // Per-scenario factor cache (null fac: off).  The Schur complement and its
+    // inverse factor depend on A (fixed), the active set (column and row codes)
+    // and the prox weights pN + the regularisation; they change little from one
+    // PH iteration to the next, so the factor of the last set a scenario solved
+    // with is kept (its explicit L^-1 and 1/diag) under that key and reused
+    // when a round's active set and weights match it bit for bit.
+    double* fac;          // [S][fac_stride]: L^-1 (ma x ld, rows) then dg (ma)
+    int64_t fac_stride;
+    int8_t* key;          // [S][key_stride]: column codes (n) then row codes (m)
+    int64_t key_stride;
+    double* pkey;         // [S][N+1]: pN of the nonant slots, then reg
+    int32_t* ok;          // [S]: the cached factor is valid
+    int32_t N;
 };
 
 // Carve of the dynamic LDS of one scenario.
@@ -210,77 +223,116 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
         const int ma = wg_compact(L, m);
         if (WG_TID == 0) { L.flag[0] = 0; L.flag[1] = 0; L.flag[2] = 0; }
         WG_SYNC();
-        // ---- Schur complement A_RF (P_FF+reg)^-1 A_RF' + reg I (lower part).
-        //      Row stride ld = ma | 1 (odd): a wavefront reading one column of
-        //      64 rows hits distinct LDS banks (an even stride of 40 doubles
-        //      made that a 16-way conflict) ----
         const int ld = ma | 1;
-        for (int e = WG_TID; e < ma * ld; e += WG_NT) {
-            const int i = e / ld, k = e - i * ld;
-            L.Sm[e] = (i == k) ? reg : 0.0;
-        }
-        WG_SYNC();
-        for (int p = WG_TID; p < G.npair; p += WG_NT) {
-            const int pa = L.pos[G.ia[p]], pb = L.pos[G.ib[p]];
-            if (pa < 0 || pb < 0) continue;
-            double v = 0.0;
-            for (int t = G.ptr[p]; t < G.ptr[p + 1]; ++t) {
-                const int ka = G.ka[t], j = ci[ka];
-                if (L.cc[j] == 0) v += L.a[ka] * L.a[G.kb[t]] / (L.pp[j] + reg);
-            }
-            L.Sm[pa * ld + pb] += v;
-        }
-        WG_SYNC();
-        WG_TP(1);
-        // ---- Cholesky: trailing update on the lower part, L[i][k] (i > k)
-        //      stored transposed at Sm[k*ld+i], 1/diagonal in dg ----
-        bool spd = true;
-        for (int jj = 0; jj < ma; ++jj) {
-            const double d = L.Sm[jj * ld + jj];
-            if (!(d > 0.0)) { spd = false; break; }
-            const double sd = sqrt(d), id = 1.0 / d;
-            for (int i = jj + 1 + WG_TID; i < ma; i += WG_NT) {
-                double* row = L.Sm + (size_t)i * ld;
-                const double lij = row[jj];
-                L.Sm[jj * ld + i] = lij / sd;
-                const double f = lij * id;
-                int k = jj + 1;
-                // batches of 4: all loads issued before the stores (LDS
-                // pointers may alias as far as the compiler knows)
-                for (; k + 3 <= i; k += 4) {
-                    const double g0 = L.Sm[k * ld + jj], g1 = L.Sm[(k + 1) * ld + jj];
-                    const double g2 = L.Sm[(k + 2) * ld + jj], g3 = L.Sm[(k + 3) * ld + jj];
-                    const double r0 = row[k], r1 = row[k + 1], r2 = row[k + 2], r3 = row[k + 3];
-                    row[k] = r0 - f * g0; row[k + 1] = r1 - f * g1;
-                    row[k + 2] = r2 - f * g2; row[k + 3] = r3 - f * g3;
-                }
-                for (; k <= i; ++k) row[k] -= f * L.Sm[k * ld + jj];
-            }
-            if (WG_TID == 0) L.dg[jj] = 1.0 / sd;
+        // ---- the cached factor of this active set and prox weights, if any ----
+        const bool cache = G.fac != nullptr;
+        bool reused = false;
+        if (cache && G.ok[s]) {
+            const int8_t* kc = G.key + (int64_t)s * G.key_stride;
+            const double* pk = G.pkey + (int64_t)s * (G.N + 1);
+            bool diff = false;
+            for (int j = WG_TID; j < n; j += WG_NT) diff = diff || kc[j] != L.cc[j];
+            for (int i = WG_TID; i < m; i += WG_NT) diff = diff || kc[n + i] != L.rc[i];
+            for (int t = WG_TID; t < G.N; t += WG_NT) diff = diff || pk[t] != P.pN[ix(t, s, S)];
+            if (WG_TID == 0 && pk[G.N] != reg) diff = true;
+            if (diff) L.flag[1] = 1;
             WG_SYNC();
-        }
-        if (!spd) return 0;
-        WG_TP(2);
-        // ---- explicit inverse of L into the lower part (diagonal included):
-        //      one column per thread, no cross-thread dependence ----
-        for (int c = WG_TID; c < ma; c += WG_NT) {
-            L.Sm[c * ld + c] = L.dg[c];
-            for (int i = c + 1; i < ma; ++i) {
-                // four partial sums: four LDS load pairs in flight per step
-                double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
-                int k = c;
-                for (; k + 3 < i; k += 4) {
-                    v0 += L.Sm[k * ld + i] * L.Sm[k * ld + c];
-                    v1 += L.Sm[(k + 1) * ld + i] * L.Sm[(k + 1) * ld + c];
-                    v2 += L.Sm[(k + 2) * ld + i] * L.Sm[(k + 2) * ld + c];
-                    v3 += L.Sm[(k + 3) * ld + i] * L.Sm[(k + 3) * ld + c];
-                }
-                for (; k < i; ++k) v0 += L.Sm[k * ld + i] * L.Sm[k * ld + c];
-                L.Sm[i * ld + c] = -((v0 + v1) + (v2 + v3)) * L.dg[i];
+            if (L.flag[1] == 0) {
+                const double* f = G.fac + (int64_t)s * G.fac_stride;
+                for (int e = WG_TID; e < ma * ld; e += WG_NT) L.Sm[e] = f[e];
+                for (int e = WG_TID; e < ma; e += WG_NT) L.dg[e] = f[(int64_t)ma * ld + e];
+                WG_SYNC();
+                WG_CNT(10);
+                reused = true;
             }
         }
-        WG_SYNC();
-        WG_TP(3);
+        if (!reused) {
+            // ---- Schur complement A_RF (P_FF+reg)^-1 A_RF' + reg I (lower part).
+            //      Row stride ld = ma | 1 (odd): a wavefront reading one column of
+            //      64 rows hits distinct LDS banks (an even stride of 40 doubles
+            //      made that a 16-way conflict) ----
+            for (int e = WG_TID; e < ma * ld; e += WG_NT) {
+                const int i = e / ld, k = e - i * ld;
+                L.Sm[e] = (i == k) ? reg : 0.0;
+            }
+            WG_SYNC();
+            for (int p = WG_TID; p < G.npair; p += WG_NT) {
+                const int pa = L.pos[G.ia[p]], pb = L.pos[G.ib[p]];
+                if (pa < 0 || pb < 0) continue;
+                double v = 0.0;
+                for (int t = G.ptr[p]; t < G.ptr[p + 1]; ++t) {
+                    const int ka = G.ka[t], j = ci[ka];
+                    if (L.cc[j] == 0) v += L.a[ka] * L.a[G.kb[t]] / (L.pp[j] + reg);
+                }
+                L.Sm[pa * ld + pb] += v;
+            }
+            WG_SYNC();
+            WG_TP(1);
+            // ---- Cholesky: trailing update on the lower part, L[i][k] (i > k)
+            //      stored transposed at Sm[k*ld+i], 1/diagonal in dg ----
+            bool spd = true;
+            for (int jj = 0; jj < ma; ++jj) {
+                const double d = L.Sm[jj * ld + jj];
+                if (!(d > 0.0)) { spd = false; break; }
+                const double sd = sqrt(d), id = 1.0 / d;
+                for (int i = jj + 1 + WG_TID; i < ma; i += WG_NT) {
+                    double* row = L.Sm + (size_t)i * ld;
+                    const double lij = row[jj];
+                    L.Sm[jj * ld + i] = lij / sd;
+                    const double f = lij * id;
+                    int k = jj + 1;
+                    // batches of 4: all loads issued before the stores (LDS
+                    // pointers may alias as far as the compiler knows)
+                    for (; k + 3 <= i; k += 4) {
+                        const double g0 = L.Sm[k * ld + jj], g1 = L.Sm[(k + 1) * ld + jj];
+                        const double g2 = L.Sm[(k + 2) * ld + jj], g3 = L.Sm[(k + 3) * ld + jj];
+                        const double r0 = row[k], r1 = row[k + 1], r2 = row[k + 2], r3 = row[k + 3];
+                        row[k] = r0 - f * g0; row[k + 1] = r1 - f * g1;
+                        row[k + 2] = r2 - f * g2; row[k + 3] = r3 - f * g3;
+                    }
+                    for (; k <= i; ++k) row[k] -= f * L.Sm[k * ld + jj];
+                }
+                if (WG_TID == 0) L.dg[jj] = 1.0 / sd;
+                WG_SYNC();
+            }
+            if (!spd) return 0;
+            WG_TP(2);
+            // ---- explicit inverse of L into the lower part (diagonal included):
+            //      one column per thread, no cross-thread dependence ----
+            for (int c = WG_TID; c < ma; c += WG_NT) {
+                L.Sm[c * ld + c] = L.dg[c];
+                for (int i = c + 1; i < ma; ++i) {
+                    // four partial sums: four LDS load pairs in flight per step
+                    double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
+                    int k = c;
+                    for (; k + 3 < i; k += 4) {
+                        v0 += L.Sm[k * ld + i] * L.Sm[k * ld + c];
+                        v1 += L.Sm[(k + 1) * ld + i] * L.Sm[(k + 1) * ld + c];
+                        v2 += L.Sm[(k + 2) * ld + i] * L.Sm[(k + 2) * ld + c];
+                        v3 += L.Sm[(k + 3) * ld + i] * L.Sm[(k + 3) * ld + c];
+                    }
+                    for (; k < i; ++k) v0 += L.Sm[k * ld + i] * L.Sm[k * ld + c];
+                    L.Sm[i * ld + c] = -((v0 + v1) + (v2 + v3)) * L.dg[i];
+                }
+            }
+            WG_SYNC();
+            WG_TP(3);
+            if (cache) {
+                // keep this set's factor for the next solve of the scenario
+                double* f = G.fac + (int64_t)s * G.fac_stride;
+                for (int e = WG_TID; e < ma * ld; e += WG_NT) f[e] = L.Sm[e];
+                for (int e = WG_TID; e < ma; e += WG_NT) f[(int64_t)ma * ld + e] = L.dg[e];
+                int8_t* kc = G.key + (int64_t)s * G.key_stride;
+                double* pk = G.pkey + (int64_t)s * (G.N + 1);
+                for (int j = WG_TID; j < n; j += WG_NT) kc[j] = L.cc[j];
+                for (int i = WG_TID; i < m; i += WG_NT) kc[n + i] = L.rc[i];
+                for (int t = WG_TID; t < G.N; t += WG_NT) pk[t] = P.pN[ix(t, s, S)];
+                if (WG_TID == 0) {
+                    pk[G.N] = reg;
+                    G.ok[s] = 1;
+                }
+            }
+        }
         // ---- iterative refinement on the unregularised KKT (a proximal-point
         //      iteration) ----
         for (int it = 0; it < O.refine_steps; ++it) {

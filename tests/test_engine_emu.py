@@ -336,3 +336,27 @@ def check_reductions_by_iteration(lib, device, S, fused, K=3, rho=1.0):
 @pytest.mark.parametrize("fused", [0, 1])
 def test_reductions_by_iteration_emu(emu, fused):
     check_reductions_by_iteration(emu, "cpu", 3000, fused)
+
+
+def check_wg_factor_cache(lib, device, monkeypatch, S=60, iters=6):
+    """The workgroup warm solver's factor cache (phx_wg.h WgPairs::fac: the
+    factor of the last active set reused while the set and the prox weights are
+    unchanged) gives the PH trajectory of recomputing every factor, bit for bit
+    (farmer crops_multiplier=10: n = 120, above the lane solver's limits)."""
+    kw = {"num_scens": S, "crops_multiplier": 10}
+    out = []
+    for off in (False, True):
+        if off:
+            monkeypatch.setenv("PHX_WG_NO_FACTOR_CACHE", "1")
+        ph, conv, Eobj, tb = run_engine(farmer.scenario_creator, farmer.scenario_names_creator(S), kw, iters,
+                                        lib=lib, device=device)
+        assert all_certified(ph)
+        assert ("factor cache" in ph._native.jit_info(ph._ctx).decode()) != off
+        out.append((ph.W_array(), ph.xbar_by_node()["ROOT"][0], conv, Eobj))
+    monkeypatch.delenv("PHX_WG_NO_FACTOR_CACHE")
+    (W0, x0, c0, E0), (W1, x1, c1, E1) = out
+    assert np.array_equal(W0, W1) and np.array_equal(x0, x1) and c0 == c1 and E0 == E1
+
+
+def test_wg_factor_cache_emu(emu, monkeypatch):
+    check_wg_factor_cache(emu, "cpu", monkeypatch)

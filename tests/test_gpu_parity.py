@@ -393,3 +393,10 @@ def test_native_rccl_path_one_rank_gpu(gpu_lib, fused):
     (W0, x0, c0, E0), (W1, x1, c1, E1) = res
     assert rel(W1, W0) < 1e-12 and rel(x1, x0) < 1e-12
     assert rel(c1, c0) < 1e-12 and rel(E1, E0) < 1e-12
+
+
+def test_wg_factor_cache_gpu(gpu_lib, monkeypatch):
+    """k_wg_warm's factor cache reproduces the recomputed-factor trajectory bit for bit
+    (farmer crops_multiplier=10)."""
+    from test_engine_emu import check_wg_factor_cache
+    check_wg_factor_cache(gpu_lib, None, monkeypatch, S=1000, iters=6)
