@@ -277,6 +277,7 @@ def timed_run(ph, K, dev):
     t0 = time.perf_counter()
     if ev:
         ev[0].record()
+    ph._defer_iter0_checks = True          # as PH.ph_main does
     ph.Iter0()
     # (no synchronize between Iter0 and iterk_loop -- ph_main has none: the
     # Iter0 share is the device time between two events on the same stream,

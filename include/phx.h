@@ -290,7 +290,8 @@ typedef int (*phx_allreduce_fn)(void* user, double* buf, int64_t count, void* st
  * count travels in the all-reduced node sums); the host finishes those lanes
  * and resumes, so every iteration sees final x exactly as the Python loop.
  * Requires the lane solver (phx_jit_info "on"), no phx_set_bounds override,
- * a finished previous solve, and segments that partition the local
+ * a previous solve that is finished or a pending deferred lane-solver solve
+ * (adopted, see phx_iterk_result.adopted), and segments that partition the local
  * scenarios.  W is updated in place.  The PH terms are those of the last
  * phx_set_ph_terms (W, rho, xbar_node must be the arrays given here).       */
 typedef struct phx_iterk_args {
@@ -314,6 +315,11 @@ typedef struct phx_iterk_args {
     int32_t node_stage_len;          /* doubles in node_stage; >= 2*NNS+1+conv_R enables the
                                         fused mode (one launch per PH iteration, two-stage
                                         trees): the all-reduce then carries the conv sums too */
+    double* iter0_obj;               /* [S] or NULL: when phx_iterk adopts a pending deferred
+                                        solve (Iter0's), its final objectives and statuses are
+                                        copied here for the caller's Iter0 expectations (E1,
+                                        feas_prob, trivial bound: phbase.py:805-856)         */
+    int32_t* iter0_status;           /* [S] or NULL                                          */
 } phx_iterk_args;
 
 typedef struct phx_iterk_result {
@@ -328,6 +334,11 @@ typedef struct phx_iterk_result {
     int32_t warm_launches;
     double wall_ms;
     int32_t fused;         /* 1: the fused one-launch-per-iteration mode ran     */
+    int32_t adopted;       /* 1: a pending deferred lane-solver solve (Iter0's) was
+                              adopted as the solve before iteration 1 -- enqueued
+                              behind without a host round trip; phx_last_solve_stats
+                              then reports that solve                           */
+    int32_t adopted_stragglers; /* its lanes finished on the generic path      */
 } phx_iterk_result;
 
 int phx_iterk(phx_ctx* ctx, const phx_solve_opts* opts, const phx_iterk_args* args,

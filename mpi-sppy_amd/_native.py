@@ -82,6 +82,7 @@ class IterkArgs(ctypes.Structure):
         ("conv_counts_host", c_void_p), ("conv_R", c_int32), ("convthresh", c_double),
         ("max_iters", c_int32), ("depth", c_int32), ("timing", c_int32),
         ("allreduce", ALLREDUCE_FN), ("allreduce_user", c_void_p), ("node_stage_len", c_int32),
+        ("iter0_obj", c_void_p), ("iter0_status", c_void_p),
     ]
 
 
@@ -90,6 +91,7 @@ class IterkResult(ctypes.Structure):
         ("iters", c_int32), ("converged", c_int32), ("conv", c_double), ("solves", c_int32),
         ("straggler_stops", c_int32), ("stragglers", c_int32), ("not_optimal", c_int32),
         ("warm_ms", c_double), ("warm_launches", c_int32), ("wall_ms", c_double), ("fused", c_int32),
+        ("adopted", c_int32), ("adopted_stragglers", c_int32),
     ]
 
 

@@ -313,8 +313,72 @@ class PHBase(SPOpt):
             self._reenable_prox()
 
     # ------------------------------------------------------------ loops
+    def _can_defer_iter0(self):
+        """Iter0's checks (E1, feasibility, trivial bound) may wait for the device
+        loop: ph_main asked for it, nothing observes the state between Iter0 and
+        the first iteration (no hooks, converger, hub, rho setter, printouts), and
+        the iterations will run in phx_iterk, which then adopts Iter0's deferred
+        solve (no host round trip between them)."""
+        if not getattr(self, "_defer_iter0_checks", False):
+            return False
+        if (self.extensions is not None or self.ph_converger is not None or self.spcomm is not None
+                or self.rho_setter is not None):
+            return False
+        o = self.options
+        if o["display_progress"] or o["verbose"] or o["display_convergence_detail"] or o["display_timing"]:
+            return False
+        if int(o["PHIterLimit"]) < 1:
+            return False
+        saved = self.current_solver_options
+        self.current_solver_options = self.options["iterk_solver_options"]
+        try:
+            return self._native_loop_ok()
+        finally:
+            self.current_solver_options = saved
+
+    def _iter0_checks(self, v):
+        """phbase.py:805-856 on the sums [sum p obj, sum p, sum p [optimal]] of
+        Iter0's solve: E1 and feasibility (quit() on failure), trivial bound."""
+        self.E1 = float(v[1])
+        if abs(1 - self.E1) > self.E1_tolerance:
+            if self.cylinder_rank == 0:
+                print("ERROR")
+                print("Total probability of scenarios was ", self.E1)
+                print("E1_tolerance = ", self.E1_tolerance)
+            quit()
+        feasP = float(v[2])
+        if feasP != self.E1:
+            if self.cylinder_rank == 0:
+                print("ERROR")
+                print("Infeasibility detected; E_feas, E1=", feasP, self.E1)
+            quit()
+        sgn = 1.0 if self.is_minimizing else -1.0
+        self.trivial_bound = sgn * (float(v[0]) + self._pc0_all())
+
+    def _resolve_deferred_iter0(self):
+        """The deferred Iter0 checks, on Iter0's objectives / statuses (copied by
+        phx_iterk when it adopted the solve, else by Iter0 or here)."""
+        self._iter0_deferred = False
+        if self._solve_pending:
+            # not adopted (the loop did not run on the device): finish it here,
+            # before anything else touches its outputs
+            self._sync_solve()
+            self._iter0_obj_dev.copy_(self._obj)
+            self._iter0_status_dev.copy_(self._status)
+        lib = self._native
+        lib.check(self._ctx, lib.expect(self._ctx, self._prob.data_ptr(), self._iter0_obj_dev.data_ptr(),
+                                        self._iter0_status_dev.data_ptr(), self._expect_buf.data_ptr(),
+                                        self._stream()), "expect")
+        self._expect_key = None
+        self._iter0_checks(self._sums_over_ranks(self._expect_buf))
+
     def Iter0(self):
-        """phbase.py:758-872."""
+        """phbase.py:758-872.  Returns the trivial bound, or None when ph_main
+        deferred Iter0's checks to the device loop (_can_defer_iter0): they run
+        right after it, before anything reads the state (ph_main returns
+        self.trivial_bound then)."""
+        if self._can_defer_iter0():
+            return self._iter0_deferred_start()
         if self.extensions is not None:
             self.extobject.pre_iter0()
         # fixedness / values as the extensions left them (phbase.py:788): what
@@ -374,6 +438,27 @@ class PHBase(SPOpt):
         self.reenable_W_and_prox()
         self.current_solver_options = self.options["iterk_solver_options"]
         return self.trivial_bound
+
+    def _iter0_deferred_start(self):
+        """Iter0 without its host synchronisation: the batched LP solve is
+        enqueued (deferred); E1 / feasibility / trivial bound are evaluated after
+        the device loop, which adopts the solve (phx_iterk)."""
+        self._save_original_nonants()
+        self._PHIter = 0
+        self._create_solvers()
+        self.solve_loop(solver_options=self.current_solver_options, gripe=True, tee=False,
+                        verbose=self.options["verbose"])
+        if not self._solve_pending:
+            # already final (nothing left to adopt): Iter0's objectives / statuses now
+            self._iter0_obj_dev.copy_(self._obj)
+            self._iter0_status_dev.copy_(self._status)
+        self._iter0_deferred = True
+        self._iter0_was_deferred = True
+        self.trivial_bound = None
+        self.conv = None
+        self.reenable_W_and_prox()
+        self.current_solver_options = self.options["iterk_solver_options"]
+        return None
 
     def _native_loop_ok(self):
         """The device-driven loop (phx_iterk) runs the same iterations when no
@@ -458,8 +543,12 @@ class PHBase(SPOpt):
     def _iterk_native(self, max_iterations):
         """iterk_loop body on the device (phx_iterk): Compute_Xbar -> Update_W ->
         convergence_diff -> stop test -> solve_loop, pipelined with a device-side
-        stop flag (phbase.py:875-979 semantics, same kernels as the host loop)."""
-        self._settle()
+        stop flag (phbase.py:875-979 semantics, same kernels as the host loop).
+        A deferred Iter0 solve still pending is adopted by phx_iterk (enqueued
+        behind it, no host round trip); Iter0's checks run right after."""
+        deferred = getattr(self, "_iter0_deferred", False)
+        if not deferred:
+            self._settle()
         self._apply_fixing()
         self._set_ph_terms()
         self._x_touched = True
@@ -476,10 +565,18 @@ class PHBase(SPOpt):
         # fused mode (one launch per PH iteration, two-stage trees) unless
         # {"iterk_fused": 0}; the library decides whether the problem allows it
         a.node_stage_len = self._node_stage.numel() if int(so_dict.get("iterk_fused", 1)) else 0
+        a.iter0_obj = self._iter0_obj_dev.data_ptr() if deferred else None
+        a.iter0_status = self._iter0_status_dev.data_ptr() if deferred else None
         res = _native.IterkResult()
         t0 = time.perf_counter()
         lib.check(self._ctx, lib.iterk(self._ctx, ctypes.byref(so), ctypes.byref(a), ctypes.byref(res),
                                        self._stream()), "iterk")
+        if deferred:
+            if res.adopted:
+                # Iter0's solve, finished inside phx_iterk (phx_last_solve_stats: its statistics)
+                self._solve_pending = False
+                self._record_solve(self.solve_stats[-1], 0, int(res.adopted_stragglers))
+            self._resolve_deferred_iter0()
         return self._iterk_finish(res, time.perf_counter() - t0)
 
     def _iterk_argstruct(self):
@@ -537,6 +634,8 @@ class PHBase(SPOpt):
         self.conv = None
         max_iterations = int(self.options["PHIterLimit"])
         self.iter_times = []
+        if getattr(self, "_iter0_deferred", False) and not self._native_loop_ok():
+            self._resolve_deferred_iter0()
         if self._native_loop_ok():
             res = self._iterk_native(max_iterations)
             if not res.converged:

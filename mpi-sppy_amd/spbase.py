@@ -379,6 +379,7 @@ class SPBase:
         self._y = torch.zeros(max(m, 1) * S, dtype=f64, device=self.device)
         self._obj = torch.zeros(S, dtype=f64, device=self.device)
         self._iter0_obj_dev = torch.zeros(S, dtype=f64, device=self.device)   # Iter0's optima (PHBase)
+        self._iter0_status_dev = torch.zeros(S, dtype=i32, device=self.device)  # ... and statuses
         # nonant slot -> column, and the original-nonant copy (SPOpt._save_original_nonants)
         self._slot_cols_dev = torch.as_tensor(self.batch.nonant.slot_col.astype(np.int64), device=self.device)
         self._orig_nonants_dev = torch.zeros((self.batch.nonant.N, S), dtype=f64, device=self.device)

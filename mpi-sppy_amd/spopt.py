@@ -271,6 +271,8 @@ class SPOpt(SPBase):
 
     def _settle(self):
         """Make solve results and W final before anything reads them."""
+        if getattr(self, "_iter0_deferred", False):
+            self._resolve_deferred_iter0()
         if self._solve_pending or getattr(self, "_w_uncommitted", False):
             self._settle_pending()
 
@@ -351,23 +353,28 @@ class SPOpt(SPBase):
         key = self._expect_key
         if getattr(self, "_expect_sums_key", None) != key:
             R, r = self.n_proc, self.cylinder_rank
-            if R == 1:
-                v = self._read_small(buf[:3])
-            else:
-                # every rank's three sums side by side (x + 0 is exact), then
-                # summed in rank order on the host: the three totals see the
-                # same order, so E1 == E_feas exactly when every scenario is
-                # feasible (a ring all-reduce orders each element differently)
-                t = torch.zeros(3 * R, dtype=torch.float64, device=self.device)
-                t[3 * r:3 * r + 3] = buf[:3]
-                self.mpicomm.allreduce_(t)
-                parts = t.cpu().numpy().reshape(R, 3)
-                v = parts[0].copy()
-                for q in range(1, R):
-                    v = v + parts[q]
+            v = self._sums_over_ranks(buf)
             self._expect_sums_val = v
             self._expect_sums_key = key
         return self._expect_sums_val
+
+    def _sums_over_ranks(self, buf):
+        """The three expectation sums of buf[:3] over all ranks, on the host."""
+        R, r = self.n_proc, self.cylinder_rank
+        if R == 1:
+            return self._read_small(buf[:3])
+        # every rank's three sums side by side (x + 0 is exact), then summed in
+        # rank order on the host: the three totals see the same order, so
+        # E1 == E_feas exactly when every scenario is feasible (a ring all-reduce
+        # orders each element differently)
+        t = torch.zeros(3 * R, dtype=torch.float64, device=self.device)
+        t[3 * r:3 * r + 3] = buf[:3]
+        self.mpicomm.allreduce_(t)
+        parts = t.cpu().numpy().reshape(R, 3)
+        v = parts[0].copy()
+        for q in range(1, R):
+            v = v + parts[q]
+        return v
 
     def _pc0_all(self):
         """sum over ranks of the local sum p * objective constant (once)."""

@@ -19,7 +19,7 @@ def main():
     f = glob.glob(d + "/**/*.db", recursive=True)[0]
     c = sqlite3.connect(f)
     cols = [r[1] for r in c.execute("pragma table_info(kernels)")]
-    grid = "grid_size_x" if "grid_size_x" in cols else None
+    grid = "grid_x" if "grid_x" in cols else ("grid_size_x" if "grid_size_x" in cols else None)
     q = "select name,start,end%s from kernels order by start" % ("," + grid if grid else "")
     ks = []
     for r in c.execute(q):

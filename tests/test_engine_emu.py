@@ -360,3 +360,42 @@ def check_wg_factor_cache(lib, device, monkeypatch, S=60, iters=6):
 
 def test_wg_factor_cache_emu(emu, monkeypatch):
     check_wg_factor_cache(emu, "cpu", monkeypatch)
+
+
+def check_deferred_iter0(lib, device, S=600, iter0_solver=None, iters=5):
+    """PH.ph_main defers Iter0's host synchronisation: its E1 / feasibility checks
+    and trivial bound run after the device loop, which adopts Iter0's pending
+    solve (phx_iterk; lanes that solve leaves to the generic path stop the
+    pipeline at iteration 1, are finished, and the loop resumes).  The result is
+    the step-by-step run's (Iter0() then iterk_loop()), bit for bit."""
+    from mpisppy_amd.opt.ph import PH
+    from helpers import ph_options
+
+    def make():
+        opts = ph_options(iters)
+        opts["iter0_solver_options"] = dict(iter0_solver or {})
+        return PH(opts, farmer.scenario_names_creator(S), farmer.scenario_creator,
+                  scenario_creator_kwargs={"num_scens": S}, _native_lib=lib, _device=device)
+    a = make()
+    ca, Ea, ta = a.ph_main()
+    assert getattr(a, "_iter0_was_deferred", False)
+    b = make()
+    b.PH_Prep()
+    b.subproblem_creation(False)
+    tb = b.Iter0()
+    assert not getattr(b, "_iter0_deferred", False) and tb is not None
+    b.iterk_loop()
+    Eb = b.post_loops()
+    assert ta == tb and ca == b.conv and Ea == Eb
+    assert np.array_equal(a.W_array(), b.W_array())
+    assert np.array_equal(a.xbar_by_node()["ROOT"][0], b.xbar_by_node()["ROOT"][0])
+    assert a.E1 == b.E1 == pytest.approx(1.0)
+    assert np.array_equal(a._iter0_obj, b._iter0_obj)
+    return a, b
+
+
+@pytest.mark.parametrize("so0", [None, {"as_rounds": 0, "ipm_max_it": 2}])
+def test_deferred_iter0_emu(emu, so0):
+    a, b = check_deferred_iter0(emu, "cpu", iter0_solver=so0)
+    if so0:
+        assert a.solve_stats[0]["stragglers"] > 0      # Iter0's leftovers finished after adoption

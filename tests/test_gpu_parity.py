@@ -400,3 +400,15 @@ def test_wg_factor_cache_gpu(gpu_lib, monkeypatch):
     (farmer crops_multiplier=10)."""
     from test_engine_emu import check_wg_factor_cache
     check_wg_factor_cache(gpu_lib, None, monkeypatch, S=1000, iters=6)
+
+
+@pytest.mark.parametrize("so0", [None, {"as_rounds": 0, "ipm_max_it": 2}])
+def test_deferred_iter0_gpu(gpu_lib, so0):
+    """ph_main's deferred Iter0 (phx_iterk adopts the pending solve; with starved
+    Iter0 solves its leftovers stop the pipeline at iteration 1 and are finished)
+    == the step-by-step run, bit for bit."""
+    from test_engine_emu import check_deferred_iter0
+    a, b = check_deferred_iter0(gpu_lib, None, S=3000, iter0_solver=so0)
+    assert a.iterk_stats["fused"]
+    if so0:
+        assert a.solve_stats[0]["stragglers"] > 0
