@@ -14,5 +14,7 @@ case "$1" in
   s2)  $J "trace:r03_s2_trace:$H --ar-probe 0" "prof:r03_s2_prof:$H --ar-probe 0" ;;
   s3)  $J "test:tests/test_gpu_parity.py -k factor_cache" "bench:r03_s3_c2:--only C2 $A" \
           "trace:r03_s3_trace:$H --ar-probe 0" ;;
+  s4)  $J "test:tests/test_gpu_parity.py -k deferred_iter0" "test:tests" "bench:r03_s4_bench:$H" \
+          "trace:r03_s4_trace:$H --ar-probe 0" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
