@@ -1161,6 +1161,87 @@ PHX_LD bool as_rounds(const LaneIO& io, int sc, ASet<PT>& a, int rounds, double*
     return false;
 }
 
+// ---------------------------------------------------------------------------
+// Iter0 seeding (phx_kernels.hip enqueue_seeded_solve): T template lanes spread
+// over the batch are solved cold first; every other lane starts its warm
+// rounds from the active set of the template whose scenario data are nearest
+// to its own -- the scenario-varying numbers (A values, and c / bounds / row
+// bounds where they vary), each coordinate divided by its range over the
+// templates, squared distance.  Templates that did not certify (status != 1)
+// are skipped; -1 if none did.  The loop over templates is wave-uniform, so the
+// template data are scalar loads.
+// ---------------------------------------------------------------------------
+constexpr int SEED_T_MAX = 64;    // template lanes at most (one wavefront)
+
+template <class PT>
+PHX_LD int seed_coords() {
+    return PT::nvar() + (PT::c_vary() ? PT::n() : 0) + (PT::bnd_vary() ? 2 * PT::n() : 0) +
+           (PT::rhs_vary() ? 2 * PT::m() : 0);
+}
+
+template <class PT>
+PHX_LD double seed_coord(const LaneIO& io, int e, int sc) {
+    const int64_t S = io.S;
+    if (e < PT::nvar()) return io.Av[(int64_t)e * S + sc];
+    e -= PT::nvar();
+    if (PT::c_vary()) {
+        if (e < PT::n()) return io.c[(int64_t)e * S + sc];
+        e -= PT::n();
+    }
+    if (PT::bnd_vary()) {
+        if (e < PT::n()) return io.lb[(int64_t)e * S + sc];
+        e -= PT::n();
+        if (e < PT::n()) return io.ub[(int64_t)e * S + sc];
+        e -= PT::n();
+    }
+    if (e < PT::m()) return io.bl[(int64_t)e * S + sc];
+    return io.bu[(int64_t)(e - PT::m()) * S + sc];
+}
+
+template <class PT>
+PHX_LD int nearest_template(const LaneIO& io, int sc, const int32_t* tl, int T) {
+    constexpr int NCMAX = PT::NMAX_V + 3 * PT::NMAX_N + 2 * PT::NMAX_M;   // (entries past NC are dead)
+    const int NC = seed_coords<PT>();
+    int best = -1;
+    double bd = 0.0;
+    double mine[NCMAX], irange[NCMAX];
+    PHX_UNROLL for (int e = 0; e < NC; ++e) {
+        mine[e] = seed_coord<PT>(io, e, sc);
+        double lo = 1e300, hi = -1e300;
+        for (int k = 0; k < T; ++k) {
+            const double v = seed_coord<PT>(io, e, tl[k]);
+            lo = fmin(lo, v);
+            hi = fmax(hi, v);
+        }
+        // (infinite bounds: inf - inf = nan, a coordinate that never differs)
+        const double r = hi - lo;
+        irange[e] = (r > 0.0 && r < 1e300) ? 1.0 / r : 0.0;
+    }
+    for (int k = 0; k < T; ++k) {
+        const int t = tl[k];
+        if (io.status[t] != 1) continue;
+        double d = 0.0;
+        PHX_UNROLL for (int e = 0; e < NC; ++e) {
+            const double v = (seed_coord<PT>(io, e, t) - mine[e]) * irange[e];
+            d += v == v ? v * v : 0.0;
+        }
+        if (best < 0 || d < bd) { best = k; bd = d; }
+    }
+    return best;
+}
+
+// The lane's starting active set: the nearest certified template's words (the
+// templates' active sets saved by k_aset_save, [T][words]); unchanged if none.
+template <class PT>
+PHX_LD void seed_fill(const LaneIO& io, int sc, const int32_t* tl, int T, const uint32_t* tmpl) {
+    const int k = nearest_template<PT>(io, sc, tl, T);
+    if (k < 0) return;
+    constexpr int NW = aset_words(PT::NMAX_N, PT::NMAX_M);
+    const int nw = aset_words(PT::n(), PT::m());
+    (void)NW;
+    for (int w = 0; w < nw; ++w) io.aset[(int64_t)w * io.S + sc] = tmpl[(int64_t)k * nw + w];
+}
+
 // Certified lane: unscaled outputs, objective (incl. PH terms), active set.
 template <class PT>
 PHX_LD void write_certified(const LaneIO& io, const Data<PT>& D, int sc, const ASet<PT>& a, const double* xp,

@@ -47,7 +47,7 @@ SOLVER_DEFAULTS = {
     "wg_warm": 16,
     "sp": 1,
     "sp_rounds": 16,
-    "seed_templates": 1,
+    "seed_templates": 64,
     "rescue_rounds": 0,
 }
 
