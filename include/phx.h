@@ -320,6 +320,14 @@ typedef struct phx_iterk_args {
                                         copied here for the caller's Iter0 expectations (E1,
                                         feas_prob, trivial bound: phbase.py:805-856)         */
     int32_t* iter0_status;           /* [S] or NULL                                          */
+    const double* iter0_prob;        /* [S] or NULL: with iter0_expect, phx_iterk also enqueues
+                                        phx_expect of the adopted solve (sum p obj, sum p,
+                                        sum p [optimal]) into iter0_expect [3] (device) and
+                                        copies it to iter0_expect_host [3] (pinned host memory,
+                                        final when phx_iterk returns): Iter0's checks without
+                                        a kernel launch or a device read after the loop     */
+    double* iter0_expect;
+    double* iter0_expect_host;
 } phx_iterk_args;
 
 typedef struct phx_iterk_result {

@@ -83,6 +83,7 @@ class IterkArgs(ctypes.Structure):
         ("max_iters", c_int32), ("depth", c_int32), ("timing", c_int32),
         ("allreduce", ALLREDUCE_FN), ("allreduce_user", c_void_p), ("node_stage_len", c_int32),
         ("iter0_obj", c_void_p), ("iter0_status", c_void_p),
+        ("iter0_prob", c_void_p), ("iter0_expect", c_void_p), ("iter0_expect_host", c_void_p),
     ]
 
 

@@ -255,11 +255,10 @@ inline std::string lane_kernel_source(const LaneStructure& L, int warm_waves = 1
          "  }\n"
          "}\n";
     // Iter0 seeding: every lane takes the active set of its nearest certified
-    // template (phx_lane.h seed_fill)
+    // template (phx_lane.h seed_block: the template table staged in LDS)
     o << "extern \"C\" __global__ void __launch_bounds__(64) phx_lane_seed(phx_lane::LaneIO io, "
          "const int* tl, int T, const unsigned* tmpl) {\n"
-         "  const int t = blockIdx.x * 64 + threadIdx.x;\n"
-         "  if (t < io.S) phx_lane::seed_fill<PT>(io, t, tl, T, tmpl);\n"
+         "  phx_lane::seed_block<PT>(io, tl, T, tmpl);\n"
          "}\n";
     // the cold solve: the interior point (phx_lane_cold), then over the same
     // lanes the classification + active-set rounds (phx_lane_cold_as), which

@@ -1174,7 +1174,7 @@ PHX_LD bool as_rounds(const LaneIO& io, int sc, ASet<PT>& a, int rounds, double*
 constexpr int SEED_T_MAX = 64;    // template lanes at most (one wavefront)
 
 template <class PT>
-PHX_LD int seed_coords() {
+PHX_LD constexpr int seed_coords() {
     return PT::nvar() + (PT::c_vary() ? PT::n() : 0) + (PT::bnd_vary() ? 2 * PT::n() : 0) +
            (PT::rhs_vary() ? 2 * PT::m() : 0);
 }
@@ -1196,6 +1196,15 @@ PHX_LD double seed_coord(const LaneIO& io, int e, int sc) {
     }
     if (e < PT::m()) return io.bl[(int64_t)e * S + sc];
     return io.bu[(int64_t)(e - PT::m()) * S + sc];
+}
+
+constexpr int SEED_LDS = 4096;
+
+template <class PT>
+PHX_LD constexpr int seed_templates_staged() {
+    return seed_coords<PT>() == 0 ? SEED_T_MAX
+                                  : (SEED_T_MAX * seed_coords<PT>() <= SEED_LDS ? SEED_T_MAX
+                                                                                : SEED_LDS / seed_coords<PT>());
 }
 
 template <class PT>
@@ -1234,7 +1243,8 @@ PHX_LD int nearest_template(const LaneIO& io, int sc, const int32_t* tl, int T) 
 // templates' active sets saved by k_aset_save, [T][words]); unchanged if none.
 template <class PT>
 PHX_LD void seed_fill(const LaneIO& io, int sc, const int32_t* tl, int T, const uint32_t* tmpl) {
-    const int k = nearest_template<PT>(io, sc, tl, T);
+    const int TS = seed_templates_staged<PT>();
+    const int k = nearest_template<PT>(io, sc, tl, T < TS ? T : TS);
     if (k < 0) return;
     constexpr int NW = aset_words(PT::NMAX_N, PT::NMAX_M);
     const int nw = aset_words(PT::n(), PT::m());
@@ -1616,6 +1626,61 @@ __device__ void fz_epilogue(const LaneIO& io, int sc, bool still) {
                 (double)__hip_atomic_load(io.count_out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
+}
+
+// Iter0 seeding on the GPU (kernel phx_lane_seed, one wavefront per block):
+// the same choice as seed_fill / nearest_template, with the template table
+// staged once per block in LDS.  Read per lane from global memory, the T x NC
+// template coordinates were dependent scalar loads through the template list
+// (tl[k], then the value): 124 us for farmer 100k; from LDS, broadcast reads.
+// Ranges over all T templates, distances over the certified ones, e ascending:
+// the same floating-point sums as nearest_template.  At most SEED_LDS doubles
+// are staged: problems with more coordinates per template use fewer templates
+// (the first SEED_LDS / NC; the host emulation applies the same cap).
+template <class PT>
+__device__ void seed_block(const LaneIO& io, const int32_t* tl, int T, const uint32_t* tmpl) {
+    constexpr int NC = seed_coords<PT>();
+    constexpr int TS = seed_templates_staged<PT>() > 0 ? seed_templates_staged<PT>() : 1;
+    constexpr int NCP = NC > 0 ? NC : 1;
+    __shared__ double tc[TS * NCP];
+    __shared__ double irange[NCP];
+    __shared__ int tok[TS];
+    const int Tn = T < TS ? T : TS;
+    for (int i = threadIdx.x; i < Tn * NC; i += blockDim.x) {
+        const int k = i / NCP, e = i - k * NCP;
+        tc[i] = seed_coord<PT>(io, e, tl[k]);
+    }
+    for (int k = threadIdx.x; k < Tn; k += blockDim.x) tok[k] = io.status[tl[k]] == 1;
+    __syncthreads();
+    for (int e = threadIdx.x; e < NC; e += blockDim.x) {
+        double lo = 1e300, hi = -1e300;
+        for (int k = 0; k < Tn; ++k) {
+            const double v = tc[k * NCP + e];
+            lo = fmin(lo, v);
+            hi = fmax(hi, v);
+        }
+        const double r = hi - lo;
+        irange[e] = (r > 0.0 && r < 1e300) ? 1.0 / r : 0.0;
+    }
+    __syncthreads();
+    const int sc = blockIdx.x * blockDim.x + threadIdx.x;
+    if (sc >= io.S) return;
+    double mine[NCP];
+    PHX_UNROLL for (int e = 0; e < NC; ++e) mine[e] = seed_coord<PT>(io, e, sc);
+    int best = -1;
+    double bd = 0.0;
+    for (int k = 0; k < Tn; ++k) {
+        if (!tok[k]) continue;
+        double d = 0.0;
+        PHX_UNROLL for (int e = 0; e < NC; ++e) {
+            const double v = (tc[k * NCP + e] - mine[e]) * irange[e];
+            d += v == v ? v * v : 0.0;
+        }
+        if (best < 0 || d < bd) { best = k; bd = d; }
+    }
+    if (best < 0) return;
+    const int nw = aset_words(PT::n(), PT::m());
+    for (int w = 0; w < nw; ++w) io.aset[(int64_t)w * io.S + sc] = tmpl[(int64_t)best * nw + w];
 }
 
 // Compact the lanes that still need work into out[0..*count): one atomic per

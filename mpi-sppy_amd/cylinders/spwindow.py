@@ -15,14 +15,47 @@ never waits for a slow reader (the hub keeps iterating while a spoke reads),
 and a reader always sees one complete write — the guarantee the MPI lock gave.
 
 Segment layout (bytes): [seq: int64 | payload: (length + 1) float64].
+
+Memory ordering: the sequence word and the payload are plain numpy stores and
+loads, with no explicit fences.  The lock is correct on the deployment host
+(x86-64, EPYC: total store order — stores become visible in program order and
+loads are not reordered with older loads), and CPython executes each store as
+a separate C call the compiler cannot move across.  ``_check_host`` refuses to
+build a window on any other architecture rather than run an unfenced seqlock
+there.
+
+Crash cleanup: every segment this process created is registered with
+``atexit`` and unlinked there if ``free`` never ran, so a spoke that dies with
+an exception does not leave its segments in /dev/shm (a SIGKILL still can; the
+names are per tag, and a new window with the same name truncates the old
+file).
 """
+import atexit
 import mmap
 import os
+import platform
 import time
 
 import numpy as np
 
 _SHM_DIR = "/dev/shm"
+_OWNED = set()          # paths of segments this process created and has not unlinked
+
+
+def _check_host():
+    m = platform.machine().lower()
+    if m not in ("x86_64", "amd64"):
+        raise RuntimeError("SPWindow's sequence lock relies on x86-64 store ordering; host is %s" % m)
+
+
+@atexit.register
+def _unlink_owned():
+    for path in list(_OWNED):
+        try:
+            os.unlink(path)
+        except FileNotFoundError:
+            pass
+        _OWNED.discard(path)
 
 
 class _Segment:
@@ -32,7 +65,9 @@ class _Segment:
     def __init__(self, name, size=None):
         self.path = os.path.join(_SHM_DIR, name)
         if size is not None:
+            _check_host()
             fd = os.open(self.path, os.O_RDWR | os.O_CREAT | os.O_TRUNC, 0o600)
+            _OWNED.add(self.path)
             os.ftruncate(fd, size)
         else:
             fd = os.open(self.path, os.O_RDWR)
@@ -46,6 +81,7 @@ class _Segment:
         self.buf.close()
 
     def unlink(self):
+        _OWNED.discard(self.path)
         os.unlink(self.path)
 
 

@@ -355,10 +355,19 @@ class PHBase(SPOpt):
         sgn = 1.0 if self.is_minimizing else -1.0
         self.trivial_bound = sgn * (float(v[0]) + self._pc0_all())
 
-    def _resolve_deferred_iter0(self):
+    def _resolve_deferred_iter0(self, device_sums=False):
         """The deferred Iter0 checks, on Iter0's objectives / statuses (copied by
-        phx_iterk when it adopted the solve, else by Iter0 or here)."""
+        phx_iterk when it adopted the solve, else by Iter0 or here).
+        device_sums: phx_iterk already evaluated the expectations of the adopted
+        solve into _expect_buf and its pinned host copy (iter0_expect_host)."""
         self._iter0_deferred = False
+        if device_sums:
+            self._expect_key = None
+            if self.n_proc == 1:
+                self._iter0_checks(self._iter0_exp_host.numpy().copy())
+            else:
+                self._iter0_checks(self._sums_over_ranks(self._expect_buf))
+            return
         if self._solve_pending:
             # not adopted (the loop did not run on the device): finish it here,
             # before anything else touches its outputs
@@ -377,6 +386,7 @@ class PHBase(SPOpt):
         deferred Iter0's checks to the device loop (_can_defer_iter0): they run
         right after it, before anything reads the state (ph_main returns
         self.trivial_bound then)."""
+        self._check_stream()
         if self._can_defer_iter0():
             return self._iter0_deferred_start()
         if self.extensions is not None:
@@ -567,6 +577,12 @@ class PHBase(SPOpt):
         a.node_stage_len = self._node_stage.numel() if int(so_dict.get("iterk_fused", 1)) else 0
         a.iter0_obj = self._iter0_obj_dev.data_ptr() if deferred else None
         a.iter0_status = self._iter0_status_dev.data_ptr() if deferred else None
+        if deferred:
+            # Iter0's expectations evaluated by phx_iterk behind the adopted solve
+            a.iter0_prob, a.iter0_expect = self._prob.data_ptr(), self._expect_buf.data_ptr()
+            a.iter0_expect_host = self._iter0_exp_host.data_ptr()
+        else:
+            a.iter0_prob = a.iter0_expect = a.iter0_expect_host = None
         res = _native.IterkResult()
         t0 = time.perf_counter()
         lib.check(self._ctx, lib.iterk(self._ctx, ctypes.byref(so), ctypes.byref(a), ctypes.byref(res),
@@ -576,7 +592,7 @@ class PHBase(SPOpt):
                 # Iter0's solve, finished inside phx_iterk (phx_last_solve_stats: its statistics)
                 self._solve_pending = False
                 self._record_solve(self.solve_stats[-1], 0, int(res.adopted_stragglers))
-            self._resolve_deferred_iter0()
+            self._resolve_deferred_iter0(device_sums=bool(res.adopted))
         return self._iterk_finish(res, time.perf_counter() - t0)
 
     def _iterk_argstruct(self):
@@ -626,6 +642,7 @@ class PHBase(SPOpt):
 
     def iterk_loop(self):
         """phbase.py:875-979."""
+        self._check_stream()
         verbose = self.options["verbose"]
         have_extensions = self.extensions is not None
         have_converger = self.ph_converger is not None

@@ -450,6 +450,8 @@ class SPBase:
         self._stream()
         if self.device.type == "cuda":
             self._pinned_small()
+        # Iter0's expectation sums as phx_iterk leaves them (pinned on GPUs)
+        self._iter0_exp_host = torch.zeros(3, dtype=f64, pin_memory=self.device.type == "cuda")
 
     def _stream(self):
         """The stream every native call is ordered on: the device's current
@@ -460,6 +462,20 @@ class SPBase:
             h = self._stream_h = (torch.cuda.current_stream(self.device).cuda_stream
                                   if self.device.type == "cuda" else 0)
         return h or None
+
+    def _check_stream(self):
+        """The torch ops between native calls (small reads, events, masks) run on
+        the device's current stream; they are ordered after the native kernels
+        only while that is still the stream cached by ``_stream``.  Checked once
+        per entry point (Iter0, iterk_loop, small reads), not per call: running
+        a built object inside another ``torch.cuda.stream(...)`` context raises
+        instead of reading stale values."""
+        if self.device.type != "cuda":
+            return
+        cur = torch.cuda.current_stream(self.device).cuda_stream
+        if cur != self._stream():
+            raise RuntimeError("phx: the current stream (0x%x) is not the stream this object was built on "
+                               "(0x%x); run it outside torch.cuda.stream(...) or build it there" % (cur, self._stream()))
 
     def _pinned_small(self):
         """64 pinned host doubles, allocated once (small device reads)."""
@@ -476,6 +492,7 @@ class SPBase:
         if self.device.type != "cuda" or k > 64:
             return t.cpu().numpy()
         pin = self._pinned_small()
+        self._check_stream()
         stream = torch.cuda.current_stream(self.device)
         pin[:k].copy_(t.reshape(-1), non_blocking=True)
         stream.synchronize()

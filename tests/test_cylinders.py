@@ -275,3 +275,22 @@ def test_window_seqlock_roundtrip():
         out = o2 = None
         a.free()
         b.free()
+
+
+def test_window_segments_unlinked_at_exit(tmp_path):
+    """A process that creates a window and dies without free() (an exception in a
+    spoke) leaves no segment behind: the atexit hook unlinks what it owns."""
+    import subprocess
+    import sys
+    tag = "x%d" % os.getpid()
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "import mpisppy_amd\n"
+            "from mpisppy_amd.cylinders.spwindow import SPWindow\n"
+            "w = SPWindow(%r, 0, 0, [4])\n"
+            "print(w._own.path)\n"
+            "raise SystemExit(3)\n") % (os.path.dirname(os.path.dirname(os.path.abspath(__file__))), tag)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 3, r.stderr
+    path = r.stdout.strip().splitlines()[-1]
+    assert path.startswith("/dev/shm/phxw_" + tag)
+    assert not os.path.exists(path)

@@ -348,14 +348,29 @@ def test_time_to_conv_gpu(gpu_lib, S):
 
 
 @pytest.mark.gpu
-def test_fenced_handoff_fused_loop_gpu(gpu_lib, monkeypatch):
+@pytest.mark.parametrize("S", [1000, 20000])
+def test_fenced_handoff_fused_loop_gpu(gpu_lib, monkeypatch, S):
     """The fused loop's inter-workgroup hand-off with agent-scope release/acquire
     fences (PHX_FENCED_HANDOFF, phx_lane.h) gives the host loop's trajectory,
-    as the default relaxed write-through hand-off does."""
+    as the default relaxed write-through hand-off does; at 20k scenarios (79
+    workgroups) every arrival shard and the top counter are used."""
     monkeypatch.setenv("PHX_LANE_DEFS", "PHX_FENCED_HANDOFF")
     from test_engine_emu import check_native_vs_host
-    a, b = check_native_vs_host(gpu_lib, None, "farmer", S=1000, fused=1)
+    a, b = check_native_vs_host(gpu_lib, None, "farmer", S=S, fused=1)
     assert a.iterk_stats["fused"]
+
+
+@pytest.mark.gpu
+def test_stream_mismatch_raises_gpu(gpu_lib):
+    """An object built on one stream and run inside torch.cuda.stream(other) raises
+    (its torch-side reads would not be ordered after the native kernels)."""
+    import torch
+    S = 30
+    ph = PH(ph_options(3), farmer.scenario_names_creator(S), farmer.scenario_creator,
+            scenario_creator_kwargs={"num_scens": S}, _native_lib=gpu_lib)
+    with torch.cuda.stream(torch.cuda.Stream()):
+        with pytest.raises(RuntimeError, match="not the stream"):
+            ph.ph_main()
 
 
 def test_native_loop_workgroup_matches_host_loop_gpu(gpu_lib):
