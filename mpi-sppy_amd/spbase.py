@@ -472,10 +472,12 @@ class SPBase:
         instead of reading stale values."""
         if self.device.type != "cuda":
             return
+        self._stream()
         cur = torch.cuda.current_stream(self.device).cuda_stream
-        if cur != self._stream():
+        if cur != self._stream_h:         # (the default stream's handle is 0)
             raise RuntimeError("phx: the current stream (0x%x) is not the stream this object was built on "
-                               "(0x%x); run it outside torch.cuda.stream(...) or build it there" % (cur, self._stream()))
+                               "(0x%x); run it outside torch.cuda.stream(...) or build it there"
+                               % (cur, self._stream_h))
 
     def _pinned_small(self):
         """64 pinned host doubles, allocated once (small device reads)."""

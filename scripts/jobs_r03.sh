@@ -16,5 +16,7 @@ case "$1" in
           "trace:r03_s3_trace:$H --ar-probe 0" ;;
   s4)  $J "test:tests/test_gpu_parity.py -k deferred_iter0" "test:tests" "bench:r03_s4_bench:$H" \
           "trace:r03_s4_trace:$H --ar-probe 0" ;;
+  s5)  $J "test:tests/test_gpu_parity.py tests/test_hydro.py" "bench:r03_s5_bench:$H" \
+          "trace:r03_s5_trace:$H --ar-probe 0" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
