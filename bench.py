@@ -79,6 +79,7 @@ def parse():
     ap.add_argument("--only", default=None, help="run one config as the headline (C2, C4, C5a, C5b)")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: test hook (gloo + the host emulation library, no GPU)")
+    ap.add_argument("--so", default=None, help="extra solver options (JSON), e.g. '{\"seed_templates\": 0}'")
     ap.add_argument("--ar-probe", type=int, default=1,
                     help="N = 1: time phx_iterk with a no-op all-reduce callback (the per-iteration host "
                          "cost of the Python collective hook)")
@@ -448,6 +449,8 @@ def main():
           "iterk_fused": args.fused}
     hl = W["C3"] if args.only is None else W[args.only]
     so.update(hl.get("so", {}))
+    if args.so:
+        so.update(json.loads(args.so))
     S = args.scens if args.only is None else hl["S"]
     cm = args.cm if args.only is None else 1
     # ---- warmup: a full untimed Iter0 + W iterations on its own object ----

@@ -108,9 +108,12 @@ typedef struct phx_solve_opts {
                                  interior point (cold) and from the previous
                                  solution (warm)                              */
     int32_t seed_templates;   /* first solve of a context (Iter0) with the lane
-                                 solver: template lanes (interior point) whose
-                                 active sets the other lanes try in turn before
-                                 their own interior point (1..8)              */
+                                 solver: template lanes (interior point, 1..64);
+                                 every other lane starts active-set rounds from
+                                 the nearest certified template's active set
+                                 before its own interior point.  0: unseeded
+                                 (the interior point on every lane, then the
+                                 rescue round budget)                          */
     int32_t rescue_rounds;    /* lane solver: active-set rounds (single changes)
                                  of the rescue pass before any interior point,
                                  and of the first warm pass after a cold solve;

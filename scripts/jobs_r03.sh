@@ -18,5 +18,8 @@ case "$1" in
           "trace:r03_s4_trace:$H --ar-probe 0" ;;
   s5)  $J "test:tests/test_gpu_parity.py tests/test_hydro.py" "bench:r03_s5_bench:$H" \
           "trace:r03_s5_trace:$H --ar-probe 0" ;;
+  s6)  $J "test:tests/test_gpu_parity.py tests/test_hydro.py" "bench:r03_s6_bench:$H" \
+          "bench:r03_s6_bench_noseed:$H --so {\"seed_templates\":0}" \
+          "trace:r03_s6_trace:$H --ar-probe 0" "trace:r03_s6_trace_noseed:$H --ar-probe 0 --so {\"seed_templates\":0}" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
