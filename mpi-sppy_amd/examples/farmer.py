@@ -16,7 +16,7 @@ import numpy as np
 
 from .. import model as lm
 from ..batch import BatchData, NonantSpec
-from ..utils import sputils
+from ..utils import rng, sputils
 
 _BASENAMES = ["BelowAverageScenario", "AverageScenario", "AboveAverageScenario"]
 _YIELD = {
@@ -63,6 +63,25 @@ def _yields(scennum, cm, seedoffset, total_perturb, rel_perturb):
                 v = v + stream.rand()
             out.append(v)
     return out
+
+
+def _yields_batch(nums, cm, seedoffset, total_perturb, rel_perturb):
+    """(S, 3 cm) yields of many scenarios, == _yields row by row.  Without
+    rel_perturb (no normal() draws) the per-scenario rand() streams come from the
+    vectorised MT19937 (utils/rng.py: bit-exact RandomState(seed).rand()); with
+    it, one RandomState per scenario as _yields."""
+    nums = np.asarray(nums, dtype=np.int64)
+    S = nums.size
+    if rel_perturb != 0 or S == 0:
+        return np.array([_yields(int(k), cm, seedoffset, total_perturb, rel_perturb) for k in nums]).reshape(S, 3 * cm)
+    base = np.array([[_YIELD[_BASENAMES[b]][c] for c in _CROPBASE] for b in range(3)])   # [base][crop]
+    if total_perturb != 0:
+        base = base * (1 + total_perturb)
+    Y = np.tile(base[nums % 3], (1, cm))                                                  # [S][i*3 + crop]
+    draw = nums // 3 != 0
+    if draw.any():
+        Y[draw] = Y[draw] + rng.first_rands(nums[draw] + seedoffset, 3 * cm)
+    return Y
 
 
 def scenario_creator(scenario_name, use_integer=False, sense=lm.minimize, crops_multiplier=1,
@@ -118,9 +137,8 @@ def batch_creator(scenario_names, use_integer=False, sense=lm.minimize, crops_mu
     nc = len(crops)
     n = 4 * nc
     DA, SUB, SUP, PUR = 0, nc, 2 * nc, 3 * nc
-    Y = np.empty((S, nc))
-    for k, nm in enumerate(scenario_names):
-        Y[k] = _yields(sputils.extract_num(nm), cm, seedoffset, total_perturb, rel_perturb)
+    Y = _yields_batch([sputils.extract_num(nm) for nm in scenario_names], cm, seedoffset, total_perturb,
+                      rel_perturb)
     base = [c.rstrip("0123456789") for c in crops]
     # rows exactly as scenario_creator + LinearModel.add_row (columns sorted)
     rowptr = [0]

@@ -25,7 +25,7 @@ import torch
 
 from . import _native
 from .spbase import SPBase
-from .views import ScenarioView
+from .views import ScenarioView, ScenarioViews
 
 SOLVER_DEFAULTS = {
     "pdhg_max_iters": 200000,
@@ -111,7 +111,7 @@ class SPOpt(SPBase):
                 self.extobject = self.extensions(self, **self.extension_kwargs)
 
     def _make_views(self):
-        self.local_scenarios = {nm: ScenarioView(self, k, nm) for k, nm in enumerate(self.local_scenario_names)}
+        self.local_scenarios = ScenarioViews(self, self.local_scenario_names)
         self.local_subproblems = self.local_scenarios
 
     # ------------------------------------------------------------ solve

@@ -9,6 +9,8 @@ attributes are light views onto the batched device tensors: reads copy the
 device array to the host once per device update (``SPBase._host``), writes to
 W / rho go straight to the device.  Nothing is materialised unless a hook asks.
 """
+from collections.abc import Mapping
+
 
 
 class _ParamData:
@@ -279,3 +281,40 @@ class ScenarioView:
     def model(self):
         m = self._opt._models
         return None if m is None else m[self.name]
+
+
+class ScenarioViews(Mapping):
+    """``local_scenarios``: name -> ScenarioView, each built on first access.
+    A million local scenarios cost ~20 us of Python objects each when built
+    eagerly (20 s at 1M); the engine itself never needs them, only hooks and
+    callers that index or iterate the dict do."""
+
+    def __init__(self, opt, names):
+        self._opt = opt
+        self._names = list(names)
+        self._index = None
+        self._built = {}
+
+    def _k(self, name):
+        if self._index is None:
+            self._index = {nm: k for k, nm in enumerate(self._names)}
+        return self._index[name]
+
+    def __getitem__(self, name):
+        v = self._built.get(name)
+        if v is None:
+            v = self._built[name] = ScenarioView(self._opt, self._k(name), name)
+        return v
+
+    def __iter__(self):
+        return iter(self._names)
+
+    def __len__(self):
+        return len(self._names)
+
+    def __contains__(self, name):
+        try:
+            self._k(name)
+            return True
+        except (KeyError, TypeError):
+            return False

@@ -21,5 +21,6 @@ case "$1" in
   s6)  $J "test:tests/test_gpu_parity.py tests/test_hydro.py" "bench:r03_s6_bench:$H" \
           "bench:r03_s6_bench_noseed:$H --so {\"seed_templates\":0}" \
           "trace:r03_s6_trace:$H --ar-probe 0" "trace:r03_s6_trace_noseed:$H --ar-probe 0 --so {\"seed_templates\":0}" ;;
+  s7)  $J "py:r03_s7_host_marks:scripts/host_marks.py 100000 20 5" "bench:r03_s7_c2:--only C2 $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
