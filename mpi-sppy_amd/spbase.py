@@ -473,7 +473,8 @@ class SPBase:
         if self.device.type != "cuda":
             return
         self._stream()
-        cur = torch.cuda.current_stream(self.device).cuda_stream
+        # (the raw handle: torch.cuda.current_stream builds a Stream object, ~7 us)
+        cur = torch._C._cuda_getCurrentRawStream(self.device.index or 0)
         if cur != self._stream_h:         # (the default stream's handle is 0)
             raise RuntimeError("phx: the current stream (0x%x) is not the stream this object was built on "
                                "(0x%x); run it outside torch.cuda.stream(...) or build it there"

@@ -22,5 +22,8 @@ case "$1" in
           "bench:r03_s6_bench_noseed:$H --so {\"seed_templates\":0}" \
           "trace:r03_s6_trace:$H --ar-probe 0" "trace:r03_s6_trace_noseed:$H --ar-probe 0 --so {\"seed_templates\":0}" ;;
   s7)  $J "py:r03_s7_host_marks:scripts/host_marks.py 100000 20 5" "bench:r03_s7_c2:--only C2 $A" ;;
+  s8)  $J "test:tests/test_gpu_parity.py tests/test_hydro.py" "bench:r03_s8_bench:$H" \
+          "trace:r03_s8_trace:$H --ar-probe 0" "py:r03_s8_host_marks:scripts/host_marks.py 100000 20 5" && \
+       PHX_LANE_STAMPS=1 $J "bench:r03_s8_stamps:$H --ar-probe 0" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
