@@ -25,5 +25,7 @@ case "$1" in
   s8)  $J "test:tests/test_gpu_parity.py tests/test_hydro.py" "bench:r03_s8_bench:$H" \
           "trace:r03_s8_trace:$H --ar-probe 0" "py:r03_s8_host_marks:scripts/host_marks.py 100000 20 5" && \
        PHX_LANE_STAMPS=1 $J "bench:r03_s8_stamps:$H --ar-probe 0" ;;
+  s9)  $J "trace:r03_s9_trace_unfused:$H --ar-probe 0 --fused 0" && \
+       PHX_FRESH_LIST=1 $J "trace:r03_s9_trace_unfused_list:$H --ar-probe 0 --fused 0" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
