@@ -33,7 +33,8 @@ Inputs resident in HBM before timing.  Extra keys:
                 one worker process per core) on a bounded sample, child process,
                 rank 0 at N = 1
   configs       (N = 1) the other BASELINE configs, each timed the same way
-                (Iter0 + K' iterations): C2 farmer crops_multiplier=10 x 1,000,
+                (Iter0 + K' iterations): C3x1M farmer x 1,000,000 (the over-cache
+                HBM configuration), C2 farmer crops_multiplier=10 x 1,000,
                 C4 aircond 10x10x10, C5a sslp_15_45 x 10,000, C5b netdes
                 network-50-30-H x 10,000 — value, steady state, dominant kernel
                 + roofline, CPU baseline
@@ -74,7 +75,7 @@ def parse():
     ap.add_argument("--cpu-scens", type=int, default=40000)
     ap.add_argument("--cpu-iters", type=int, default=6)
     ap.add_argument("--cpu-procs", type=int, default=16, help="worker processes (the GPU box's CPU share)")
-    ap.add_argument("--configs", default="all", help="'all', 'none' or a comma list of C2,C4,C5a,C5b")
+    ap.add_argument("--configs", default="all", help="'all', 'none' or a comma list of C3x1M,C2,C4,C5a,C5b")
     ap.add_argument("--config-steps", type=int, default=10, help="K' of the other configs")
     ap.add_argument("--only", default=None, help="run one config as the headline (C2, C4, C5a, C5b)")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
@@ -166,7 +167,8 @@ def sp_bytes(b):
 
 # profiles/r*_pmc_<tag>_<kernel>.json of each secondary config (scripts/pmc_summary.py
 # over the config's timed launches)
-CONFIG_PMC_TAG = {"C2": "farmercm10_1k", "C4": "aircond1k", "C5a": "sslp10k", "C5b": "netdes10k"}
+CONFIG_PMC_TAG = {"C2": "farmercm10_1k", "C4": "aircond1k", "C5a": "sslp10k", "C5b": "netdes10k",
+                  "C3x1M": "farmer1m"}
 
 
 def pmc_traffic(kernel, tag):
@@ -232,6 +234,11 @@ def workloads():
         "C3": dict(creator=farmer.scenario_creator, names=lambda S: farmer.scenario_names_creator(S),
                    kw=lambda S, cm: {"num_scens": S, "crops_multiplier": cm}, nodes=None,
                    desc="farmer crops_multiplier=%d, %d scenarios (BASELINE configs[2])"),
+        "C3x1M": dict(creator=farmer.scenario_creator, names=lambda S: farmer.scenario_names_creator(1000000),
+                      kw=lambda S, cm: {"num_scens": 1000000, "crops_multiplier": 1}, nodes=None, S=1000000,
+                      desc="farmer crops_multiplier=1, 1,000,000 scenarios on one GPU (the over-cache HBM "
+                           "configuration of configs[2]: working set > 256 MiB Infinity Cache)",
+                      cpu=None),
         "C2": dict(creator=farmer.scenario_creator, names=lambda S: farmer.scenario_names_creator(1000),
                    kw=lambda S, cm: {"num_scens": 1000, "crops_multiplier": 10}, nodes=None, S=1000,
                    desc="farmer crops_multiplier=10, 1,000 scenarios (BASELINE configs[1])",
@@ -535,7 +542,7 @@ def main():
         res["cpu_baseline"] = cpu_baseline(args, cm=cm)
     # ---- the other BASELINE configs (one GPU) ----
     if world == 1 and args.only is None and args.configs != "none":
-        names = ["C2", "C4", "C5a", "C5b"] if args.configs == "all" else args.configs.split(",")
+        names = ["C3x1M", "C2", "C4", "C5a", "C5b"] if args.configs == "all" else args.configs.split(",")
         res["configs"] = {}
         for nm in names:
             try:

@@ -17,6 +17,15 @@
 // (phx_core.h), so a certified lane is as exact as a polished PDHG lane.
 // Lanes that do not certify go to the PDHG + polish path unchanged.
 //
+// Round 3: FOUR wavefronts (256 threads) per scenario.  With one wavefront
+// the solve was a chain of LDS latencies on one SIMD (farmer cm=10 x 1,000:
+// ~1 wavefront per SIMD, nothing to hide them; ~300 k cycles per round, the
+// Cholesky's one-row-per-lane update the largest part).  Now four threads
+// share each row of the Cholesky's trailing update, of the explicit inverse's
+// column recurrences and of the L^-1 mat-vecs (interleaved columns, combined
+// with two lane shuffles inside the quad), and the reductions go through LDS
+// across the four wavefronts.
+//
 // The same code is compiled for the host by tests/emu with WG_NT = 1 (every
 // strided loop runs serially, barriers vanish): each phase writes only
 // elements it owns, and cross-thread values are exchanged only through LDS
@@ -28,13 +37,18 @@ namespace phx {
 
 #if defined(__HIP_DEVICE_COMPILE__)
 #define WG_TID ((int)threadIdx.x)
-#define WG_NT 64
+#define WG_NT 256
 #define WG_SYNC() __syncthreads()
 #else
 #define WG_TID 0
 #define WG_NT 1
 #define WG_SYNC() ((void)0)
 #endif
+// quads: four adjacent threads share one row (or column) of a dense phase
+#define WG_QN (WG_NT >= 4 ? WG_NT / 4 : 1)            // quads per workgroup
+#define WG_QID (WG_NT >= 4 ? WG_TID >> 2 : 0)         // this thread's quad
+#define WG_QL (WG_NT >= 4 ? (WG_TID & 3) : 0)         // its place in the quad
+#define WG_QW (WG_NT >= 4 ? 4 : 1)                    // threads per quad
 
 // Schur-complement entries (ia >= ib) whose rows share a column, with the CSR
 // positions (ka in row ia, kb in row ib) of every shared column, built once on
@@ -64,6 +78,7 @@ struct WgPairs {
 // Carve of the dynamic LDS of one scenario.
 struct WgLds {
     double *Sm, *dg, *a, *xp, *r1, *qq, *pp, *z, *t, *u;
+    double* red;                       // [8] cross-wavefront reductions (wg_max / wg_sum)
     // 16-bit indices (wg_lds_bytes: nnz, n, m < 32768) keep farmer cm=10's
     // carve under 40 KiB, i.e. four scenarios per CU
     int16_t *cp, *ri, *c2, *rp, *ci;   // pattern: CSC colptr/rowidx/csc2csr, CSR rowptr/colidx
@@ -74,7 +89,7 @@ struct WgLds {
 
 PHX_HD size_t wg_lds_bytes(int n, int m, int nnz) {
     if (n >= 32767 || m >= 32767 || nnz >= 32767) return ~(size_t)0;   // 16-bit indices
-    size_t b = 8 * ((size_t)m * (m + 1) + 4 * (size_t)m + (size_t)nnz + 4 * (size_t)n) + 16 +
+    size_t b = 8 * ((size_t)m * (m + 1) + 4 * (size_t)m + (size_t)nnz + 4 * (size_t)n) + 16 + 64 +
                2 * ((size_t)n + 1 + 3 * (size_t)nnz + (size_t)m + 1 + 2 * (size_t)m) + (size_t)n + (size_t)m;
     return (b + 15) & ~(size_t)15;
 }
@@ -92,6 +107,7 @@ PHX_HD WgLds wg_carve(void* base, int n, int m, int nnz) {
     L.r1 = d; d += n;
     L.qq = d; d += n;
     L.pp = d; d += n;
+    L.red = d; d += 8;
     L.flag = (int32_t*)d;
     int16_t* w = (int16_t*)(L.flag + 4);
     L.cp = w; w += n + 1;
@@ -107,10 +123,27 @@ PHX_HD WgLds wg_carve(void* base, int n, int m, int nnz) {
     return L;
 }
 
-// max over the workgroup (one wavefront: butterfly over its 64 lanes)
-PHX_HD double wg_max(double v) {
+// max over the workgroup: butterfly inside each wavefront, then the four
+// wavefront results through LDS (two barriers: red may be reused right after)
+PHX_HD double wg_max(double v, double* red) {
 #if defined(__HIP_DEVICE_COMPILE__)
     for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    v = red[0];
+    for (int w = 1; w < WG_NT / 64; ++w) v = fmax(v, red[w]);
+#else
+    (void)red;
+#endif
+    return v;
+}
+
+// sum of a value over a quad (its four threads end with the same sum)
+PHX_HD double wg_quad_sum(double v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    v += __shfl_xor(v, 1, 64);
+    v += __shfl_xor(v, 2, 64);
 #endif
     return v;
 }
@@ -135,11 +168,13 @@ PHX_HD double wg_max(double v) {
 #endif
 
 // Order-preserving list of the active rows (ar) and each row's position in it
-// (pos, -1 when inactive); returns their count, the same on every thread.
-PHX_HD int wg_compact(const WgLds& L, int m) {
+// (pos, -1 when inactive), built by the first wavefront; their count goes to
+// L.flag[3] (read by every thread after the caller's barrier).
+PHX_HD void wg_compact(const WgLds& L, int m) {
     int cnt = 0;
 #if defined(__HIP_DEVICE_COMPILE__)
     const int lane = (int)threadIdx.x;
+    if (lane >= 64) return;
     for (int base = 0; base < m; base += 64) {
         const int i = base + lane;
         const bool act = i < m && L.rc[i] != 0;
@@ -153,13 +188,14 @@ PHX_HD int wg_compact(const WgLds& L, int m) {
         }
         cnt += __popcll(b);
     }
+    if (lane == 0) L.flag[3] = cnt;
 #else
     for (int i = 0; i < m; ++i) {
         if (L.rc[i]) { L.ar[cnt] = (int16_t)i; L.pos[i] = (int16_t)cnt++; }
         else L.pos[i] = -1;
     }
+    L.flag[3] = cnt;
 #endif
-    return cnt;
 }
 
 // Returns (uniformly) the number of rounds the lane used when the point in
@@ -187,7 +223,7 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
         L.pp[j] = p;
         qm = fmax(qm, fabs(q / P.dc[j]));
     }
-    const double dtol = O.kkt_tol * (1.0 + wg_max(qm));
+    const double dtol = O.kkt_tol * (1.0 + wg_max(qm, L.red));
     const double ptol = O.kkt_tol;
     WG_SYNC();
     const int16_t *cp = L.cp, *ri = L.ri, *c2 = L.c2, *rp = L.rp, *ci = L.ci;
@@ -220,9 +256,10 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
     WG_TP(0);
     for (int round = 0; round < rounds; ++round) {
         // active rows in compact order: the Schur complement is ma x ma
-        const int ma = wg_compact(L, m);
+        wg_compact(L, m);
         if (WG_TID == 0) { L.flag[0] = 0; L.flag[1] = 0; L.flag[2] = 0; }
         WG_SYNC();
+        const int ma = L.flag[3];
         const int ld = ma | 1;
         // ---- the cached factor of this active set and prox weights, if any ----
         const bool cache = G.fac != nullptr;
@@ -270,27 +307,28 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
             WG_TP(1);
             // ---- Cholesky: trailing update on the lower part, L[i][k] (i > k)
             //      stored transposed at Sm[k*ld+i], 1/diagonal in dg ----
+            // (a quad per row: its four threads take interleaved columns k, so
+            // one pivot's update is spread over 4x as many threads; the pivot
+            // row element lij is read by all four, written by none of them)
             bool spd = true;
             for (int jj = 0; jj < ma; ++jj) {
                 const double d = L.Sm[jj * ld + jj];
                 if (!(d > 0.0)) { spd = false; break; }
                 const double sd = sqrt(d), id = 1.0 / d;
-                for (int i = jj + 1 + WG_TID; i < ma; i += WG_NT) {
+                for (int i = jj + 1 + WG_QID; i < ma; i += WG_QN) {
                     double* row = L.Sm + (size_t)i * ld;
                     const double lij = row[jj];
-                    L.Sm[jj * ld + i] = lij / sd;
                     const double f = lij * id;
-                    int k = jj + 1;
-                    // batches of 4: all loads issued before the stores (LDS
-                    // pointers may alias as far as the compiler knows)
-                    for (; k + 3 <= i; k += 4) {
-                        const double g0 = L.Sm[k * ld + jj], g1 = L.Sm[(k + 1) * ld + jj];
-                        const double g2 = L.Sm[(k + 2) * ld + jj], g3 = L.Sm[(k + 3) * ld + jj];
-                        const double r0 = row[k], r1 = row[k + 1], r2 = row[k + 2], r3 = row[k + 3];
-                        row[k] = r0 - f * g0; row[k + 1] = r1 - f * g1;
-                        row[k + 2] = r2 - f * g2; row[k + 3] = r3 - f * g3;
+                    int k = jj + 1 + WG_QL;
+                    // batches of 2 per thread: the loads issued before the stores
+                    for (; k + WG_QW <= i; k += 2 * WG_QW) {
+                        const double g0 = L.Sm[k * ld + jj], g1 = L.Sm[(k + WG_QW) * ld + jj];
+                        const double r0 = row[k], r1 = row[k + WG_QW];
+                        row[k] = r0 - f * g0;
+                        row[k + WG_QW] = r1 - f * g1;
                     }
-                    for (; k <= i; ++k) row[k] -= f * L.Sm[k * ld + jj];
+                    for (; k <= i; k += WG_QW) row[k] -= f * L.Sm[k * ld + jj];
+                    if (WG_QL == 0) L.Sm[jj * ld + i] = lij / sd;
                 }
                 if (WG_TID == 0) L.dg[jj] = 1.0 / sd;
                 WG_SYNC();
@@ -299,20 +337,21 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
             WG_TP(2);
             // ---- explicit inverse of L into the lower part (diagonal included):
             //      one column per thread, no cross-thread dependence ----
-            for (int c = WG_TID; c < ma; c += WG_NT) {
-                L.Sm[c * ld + c] = L.dg[c];
+            // (a quad per column c: interleaved k, two partial sums per thread,
+            // combined inside the quad; every thread of the quad holds the new
+            // entry and writes the same value, so the next step's reads of it
+            // by the other three need no ordering beyond their own store)
+            for (int c = WG_QID; c < ma; c += WG_QN) {
+                if (WG_QL == 0) L.Sm[c * ld + c] = L.dg[c];
                 for (int i = c + 1; i < ma; ++i) {
-                    // four partial sums: four LDS load pairs in flight per step
-                    double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
-                    int k = c;
-                    for (; k + 3 < i; k += 4) {
+                    double v0 = WG_QL == 0 ? L.Sm[c * ld + i] * L.dg[c] : 0.0, v1 = 0.0;
+                    int k = c + 1 + WG_QL;
+                    for (; k + WG_QW < i; k += 2 * WG_QW) {
                         v0 += L.Sm[k * ld + i] * L.Sm[k * ld + c];
-                        v1 += L.Sm[(k + 1) * ld + i] * L.Sm[(k + 1) * ld + c];
-                        v2 += L.Sm[(k + 2) * ld + i] * L.Sm[(k + 2) * ld + c];
-                        v3 += L.Sm[(k + 3) * ld + i] * L.Sm[(k + 3) * ld + c];
+                        v1 += L.Sm[(k + WG_QW) * ld + i] * L.Sm[(k + WG_QW) * ld + c];
                     }
-                    for (; k < i; ++k) v0 += L.Sm[k * ld + i] * L.Sm[k * ld + c];
-                    L.Sm[i * ld + c] = -((v0 + v1) + (v2 + v3)) * L.dg[i];
+                    for (; k < i; k += WG_QW) v0 += L.Sm[k * ld + i] * L.Sm[k * ld + c];
+                    L.Sm[i * ld + c] = -wg_quad_sum(v0 + v1) * L.dg[i];
                 }
             }
             WG_SYNC();
@@ -356,31 +395,29 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
             }
             WG_SYNC();
             // u = L^-1 t ; then t = L^-T u (dz, compact order)
-            for (int i = WG_TID; i < ma; i += WG_NT) {
-                double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
+            for (int i = WG_QID; i < ma; i += WG_QN) {
+                double v0 = 0.0, v1 = 0.0;
                 const double* row = L.Sm + (size_t)i * ld;
-                int k = 0;
-                for (; k + 3 <= i; k += 4) {
+                int k = WG_QL;
+                for (; k + WG_QW <= i; k += 2 * WG_QW) {
                     v0 += row[k] * L.t[k];
-                    v1 += row[k + 1] * L.t[k + 1];
-                    v2 += row[k + 2] * L.t[k + 2];
-                    v3 += row[k + 3] * L.t[k + 3];
+                    v1 += row[k + WG_QW] * L.t[k + WG_QW];
                 }
-                for (; k <= i; ++k) v0 += row[k] * L.t[k];
-                L.u[i] = (v0 + v1) + (v2 + v3);
+                for (; k <= i; k += WG_QW) v0 += row[k] * L.t[k];
+                const double v = wg_quad_sum(v0 + v1);
+                if (WG_QL == 0) L.u[i] = v;
             }
             WG_SYNC();
-            for (int k = WG_TID; k < ma; k += WG_NT) {
-                double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
-                int i = k;
-                for (; i + 3 < ma; i += 4) {
+            for (int k = WG_QID; k < ma; k += WG_QN) {
+                double v0 = 0.0, v1 = 0.0;
+                int i = k + WG_QL;
+                for (; i + WG_QW < ma; i += 2 * WG_QW) {
                     v0 += L.Sm[i * ld + k] * L.u[i];
-                    v1 += L.Sm[(i + 1) * ld + k] * L.u[i + 1];
-                    v2 += L.Sm[(i + 2) * ld + k] * L.u[i + 2];
-                    v3 += L.Sm[(i + 3) * ld + k] * L.u[i + 3];
+                    v1 += L.Sm[(i + WG_QW) * ld + k] * L.u[i + WG_QW];
                 }
-                for (; i < ma; ++i) v0 += L.Sm[i * ld + k] * L.u[i];
-                L.t[k] = (v0 + v1) + (v2 + v3);
+                for (; i < ma; i += WG_QW) v0 += L.Sm[i * ld + k] * L.u[i];
+                const double v = wg_quad_sum(v0 + v1);
+                if (WG_QL == 0) L.t[k] = v;
             }
             WG_SYNC();
             double dmax = 0.0, xmax = 0.0;
@@ -405,8 +442,8 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
                 L.z[i] = zn;
             }
             // stop once the correction vanishes (phx_lane.h kkt_refine's rule)
-            const bool done = wg_max(dmax) <= 1e-10 * (1.0 + wg_max(xmax));
-            WG_SYNC();
+            const double dmx = wg_max(dmax, L.red);
+            const bool done = dmx <= 1e-10 * (1.0 + wg_max(xmax, L.red));
             WG_CNT(8);
             if (done) break;
         }
@@ -481,10 +518,18 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
     return 0;
 }
 
-// sum over the workgroup (one wavefront: butterfly), identity on the host
-PHX_HD double wg_sum(double v) {
+// sum over the workgroup (butterflies, then the wavefronts in order through
+// LDS), identity on the host
+PHX_HD double wg_sum(double v, double* red) {
 #if defined(__HIP_DEVICE_COMPILE__)
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    v = red[0];
+    for (int w = 1; w < WG_NT / 64; ++w) v += red[w];
+#else
+    (void)red;
 #endif
     return v;
 }
@@ -504,7 +549,7 @@ PHX_HD void wg_write_out(const Prob& P, const WgLds& L, const double* c_unscaled
     }
     if (y_out)
         for (int i = WG_TID; i < P.m; i += WG_NT) y_out[ix(i, s, S)] = -L.z[i] * P.dr[i];
-    f = wg_sum(f);
+    f = wg_sum(f, L.red);
     if (WG_TID == 0) obj_out[s] = P.kN[s] + f;
 }
 

@@ -27,5 +27,9 @@ case "$1" in
        PHX_LANE_STAMPS=1 $J "bench:r03_s8_stamps:$H --ar-probe 0" ;;
   s9)  $J "trace:r03_s9_trace_unfused:$H --ar-probe 0 --fused 0" && \
        PHX_FRESH_LIST=1 $J "trace:r03_s9_trace_unfused_list:$H --ar-probe 0 --fused 0" ;;
+  s10) $J "test:tests/test_sslp.py tests/test_trajectories.py tests/test_gpu_parity.py::test_sslp_ph_gpu tests/test_gpu_parity.py::test_sslp_synthetic_batch_gpu tests/test_gpu_parity.py::test_farmer_cm10_1000_workgroup_gpu tests/test_gpu_parity.py::test_native_loop_workgroup_matches_host_loop_gpu tests/test_gpu_parity.py::test_native_loop_workgroup_stragglers_gpu tests/test_gpu_parity.py::test_wg_factor_cache_gpu" \
+          "bench:r03_s10_c2:--only C2 $A" "bench:r03_s10_c5a:--only C5a $A" \
+          "trace:r03_s9_trace_unfused:$H --ar-probe 0 --fused 0" && \
+       PHX_FRESH_LIST=1 $J "trace:r03_s9_trace_unfused_list:$H --ar-probe 0 --fused 0" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
