@@ -31,5 +31,6 @@ case "$1" in
           "bench:r03_s10_c2:--only C2 $A" "bench:r03_s10_c5a:--only C5a $A" \
           "trace:r03_s9_trace_unfused:$H --ar-probe 0 --fused 0" && \
        PHX_FRESH_LIST=1 $J "trace:r03_s9_trace_unfused_list:$H --ar-probe 0 --fused 0" ;;
+  s11) $J "test:tests" "bench:r03_s11_bench:$H" "trace:r03_s11_trace:$H --ar-probe 0" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
