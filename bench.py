@@ -366,10 +366,16 @@ def dominant_kernel(ph, K, fused):
     if st is not None and st.get("warm_launches", 0) > 0:
         # phx_iterk times its per-iteration solve kernel: the lane solver's warm
         # launch, or (subproblems above the lane limits) the workgroup pass
-        if ph._native.jit_info(ph._ctx).decode().startswith("on"):
+        info = ph._native.jit_info(ph._ctx).decode()
+        if info.startswith("on"):
             return ("phx_lane_warm", st["lane_warm_ms"] / 1e3 / st["warm_launches"], st["warm_launches"],
                     lane_bytes(b, fused=bool(st.get("fused")) and fused), b.S)
-        return ("k_wg_warm", st["lane_warm_ms"] / 1e3 / st["warm_launches"], st["warm_launches"], wg_bytes(b), b.S)
+        if "workgroup solver on" in info:
+            return ("k_wg_warm", st["lane_warm_ms"] / 1e3 / st["warm_launches"], st["warm_launches"], wg_bytes(b),
+                    b.S)
+        # the sparse solver's warm pass (the bracketed events also cover its
+        # PH-term and warm-start kernels: a few us against tens of ms)
+        return ("k_sp_solve", st["lane_warm_ms"] / 1e3 / st["warm_launches"], st["warm_launches"], sp_bytes(b), b.S)
     stats = ph.solve_stats[-K:]
     cand = {
         "phx_lane_warm": (sum(s.get("lane_warm_ms", 0.0) for s in stats), lane_bytes(b)),

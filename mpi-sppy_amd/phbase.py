@@ -491,14 +491,19 @@ class PHBase(SPOpt):
 
     def _device_loop_solver(self, so):
         """Which solve phx_iterk can run per iteration: the lane solver (jit on),
-        or, above its size limits, the workgroup warm pass (k_wg_warm)."""
+        or, above its size limits, the workgroup warm pass (k_wg_warm), or above
+        those the sparse solver's warm pass (k_sp_solve)."""
         info = getattr(self, "_jit_info", None)
         if info is None:
             info = self._jit_info = self._native.jit_info(self._ctx).decode()
         if info.startswith("on") and int(so.lane_solver):
             return True
-        return ("workgroup solver on" in info and int(so.wg_warm) > 0 and int(so.polish) > 0
-                and int(so.warm_start) > 0)
+        if int(so.polish) <= 0 or int(so.warm_start) <= 0:
+            return False
+        if "workgroup solver on" in info and int(so.wg_warm) > 0:
+            return True
+        # above the workgroup limits: the sparse solver's warm pass (netdes)
+        return "sparse solver on" in info and int(so.sp) > 0
 
     def _want_native_comm(self):
         """phx_iterk's per-iteration all-reduce from C (an RCCL communicator of

@@ -32,5 +32,6 @@ case "$1" in
           "trace:r03_s9_trace_unfused:$H --ar-probe 0 --fused 0" && \
        PHX_FRESH_LIST=1 $J "trace:r03_s9_trace_unfused_list:$H --ar-probe 0 --fused 0" ;;
   s11) $J "test:tests" "bench:r03_s11_bench:$H" "trace:r03_s11_trace:$H --ar-probe 0" ;;
+  s12) $J "test:tests" "bench:r03_s12_bench:$H" "trace:r03_s12_trace:$H --ar-probe 0" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac

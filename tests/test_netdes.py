@@ -181,3 +181,37 @@ def test_netdes50_10k_gpu(gpu_lib):
     ph = check_netdes50(gpu_lib, None, 10000, 3, [0, 1, 29, 30, 4999, 9998, 9999])
     print({k: [s[k] for s in ph.solve_stats] for k in ["sp_certified", "sp_ms", "sp_ipm_its", "sp_warm_rounds",
                                                        "pdhg_iters", "wall_s"]})
+
+
+def check_native_vs_host_sp(lib, device, inst, S, iters):
+    """Subproblems above the workgroup limits: phx_iterk runs the sparse solver's
+    warm pass per iteration (k_sp_solve, stragglers through the stop / finish /
+    resume protocol) == the host loop (phx_solve -> finish_run), bit for bit."""
+    names = netdes.scenario_names_creator(S)
+    runs = []
+    for nl in (1, 0):
+        opts = {"iterk_solver_options": {"native_loop": nl}}
+        runs.append(run_engine(netdes.scenario_creator, names, {"instance": inst}, iters, lib=lib, device=device,
+                               options=opts))
+    (a, ca, Ea, ta), (b, cb, Eb, tb_) = runs
+    assert hasattr(a, "iterk_stats") and not hasattr(b, "iterk_stats")
+    info = a._native.jit_info(a._ctx).decode()
+    assert "sparse solver on" in info and "workgroup solver on" not in info, info
+    assert a._PHIter == b._PHIter == iters
+    assert np.array_equal(a.W_array(), b.W_array())
+    assert np.array_equal(a.nonant_values(), b.nonant_values())
+    assert ca == cb and Ea == Eb and ta == tb_
+    assert all_certified(a) and all_certified(b)
+    return a, b
+
+
+def test_native_loop_sparse_matches_host_loop_emu(emu, monkeypatch):
+    monkeypatch.setenv("PHX_NO_WG", "1")             # netdes-10 would fit the workgroup solver
+    check_native_vs_host_sp(emu, "cpu", INST, 10, 3)
+
+
+@pytest.mark.gpu
+def test_native_loop_sparse_matches_host_loop_gpu(gpu_lib):
+    """C5b's loop (network-50-30-H, the 30 shipped scenarios) through phx_iterk."""
+    a, b = check_native_vs_host_sp(gpu_lib, None, INST50, 30, 4)
+    assert a.iterk_stats["iters"] == 4
