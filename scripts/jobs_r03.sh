@@ -32,6 +32,9 @@ case "$1" in
           "trace:r03_s9_trace_unfused:$H --ar-probe 0 --fused 0" && \
        PHX_FRESH_LIST=1 $J "trace:r03_s9_trace_unfused_list:$H --ar-probe 0 --fused 0" ;;
   s11) $J "test:tests" "bench:r03_s11_bench:$H" "trace:r03_s11_trace:$H --ar-probe 0" ;;
-  s12) $J "test:tests" "bench:r03_s12_bench:$H" "trace:r03_s12_trace:$H --ar-probe 0" ;;
+  s12) $J "test:tests" "bench:r03_s12_bench:$H" "trace:r03_s12_trace:$H --ar-probe 0" \
+          "bench:r03_s12_c5b:--only C5b $A" ;;
+  s13) PHX_WG_PROF=1 $J "bench:r03_s13_c2_wgprof:--only C2 $A --so {\"native_loop\":0}" && \
+       PHX_SP_GRID=64 $J "bench:r03_s13_c5b_g64:--only C5b $A" && PHX_SP_GRID=128 $J "bench:r03_s13_c5b_g128:--only C5b $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
