@@ -155,7 +155,8 @@ inline void emit_dtable(std::ostringstream& o, const char* name, const std::vect
 // (hipRTC input).
 // with_map: the warm kernels carry the affine-map paths (PHX_LANE_MAP=1);
 // without, that code is compiled out (fewer registers, no spills).
-inline std::string lane_kernel_source(const LaneStructure& L, int warm_waves = 1, bool with_map = false) {
+inline std::string lane_kernel_source(const LaneStructure& L, int warm_waves = 1, bool with_map = false,
+                                      int cold_waves = 1) {
     const std::string wl = with_map ? "phx_lane::warm_lane<PT, true>" : "phx_lane::warm_lane<PT, false>";
     std::ostringstream o;
     o << "#include \"phx_lane.h\"\n";
@@ -263,7 +264,7 @@ inline std::string lane_kernel_source(const LaneStructure& L, int warm_waves = 1
     // the cold solve: the interior point (phx_lane_cold), then over the same
     // lanes the classification + active-set rounds (phx_lane_cold_as), which
     // compacts what still needs the generic path (phx_lane.h ipm_lane)
-    o << "extern \"C\" __global__ void __launch_bounds__(64) phx_lane_cold(phx_lane::LaneIO io, "
+    o << "extern \"C\" __global__ void __launch_bounds__(64, " << cold_waves << ") phx_lane_cold(phx_lane::LaneIO io, "
          "const int* lanes, const int* count) {\n"
          "  if (phx_lane::gated(io.gate)) return;\n"
          "  const int nl = count ? *count : io.S;\n"
