@@ -13,6 +13,21 @@ import numpy as np
 from .spwindow import SPWindow
 
 
+def window_lengths(hub_lengths, spoke_lengths):
+    """Per-window owner lengths: window i (spoke i + 1) holds the hub's buffer
+    for that spoke (hub_lengths[i] payload values, owned by strata rank 0) and
+    the spoke's own buffer (spoke_lengths[i], owned by strata rank i + 1);
+    the other strata ranks own nothing in it."""
+    n = len(hub_lengths)
+    out = []
+    for i in range(n):
+        ln = [0] * (n + 1)
+        ln[0] = int(hub_lengths[i])
+        ln[i + 1] = int(spoke_lengths[i])
+        out.append(ln)
+    return out
+
+
 class SPCommunicator:
     def __init__(self, spbase_object, fullcomm, strata_comm, cylinder_comm, options=None):
         self._windows_constructed = False

@@ -1,10 +1,18 @@
-"""Spoke side of the hub-and-spoke system (cylinders/spoke.py:18-376).
+"""Spokes: the cylinders that read what the hub publishes and send bounds back
+(the reference's class hierarchy of mpisppy/cylinders/spoke.py:18-376 -- same
+class names, roles and attributes -- built here on two channel objects).
 
-Same class hierarchy and wire format as the reference: a spoke owns one buffer
-``[bound | write_id]`` (spoke -> hub) and reads the hub's ``[payload | outer,
-inner, write_id]`` (hub -> spoke); ``spoke_from_hub`` accepts a read only when
-every cylinder rank saw the same write id (max == min over the cylinder,
-spoke.py:84-118), and ``write_id == -1`` is the kill signal.
+A spoke owns one window (the one of its strata rank):
+
+* ``to_hub``   an ``Outbox`` it owns: ``[bound | write_id]`` (one value);
+* ``from_hub`` an ``Inbox`` the hub owns: ``[payload | outer, inner, write_id]``,
+  where the payload is W or the nonants of this rank's scenarios (scenario-major,
+  the reference's flat layout) or empty for bound-only spokes.
+
+The class decides the payload by its roles (``converger_spoke_types``), the
+hub reads the same roles to decide what to publish (hub.py).  Every poll of
+the hub's buffer goes through ``got_kill_signal()``; ``new_Ws`` /
+``new_nonants`` report whether that poll brought a new vector.
 """
 import enum
 import math
@@ -13,7 +21,8 @@ import time
 
 import numpy as np
 
-from .spcommunicator import SPCommunicator
+from .channel import Inbox, Outbox
+from .spcommunicator import SPCommunicator, window_lengths
 
 
 class ConvergerSpokeType(enum.Enum):
@@ -24,134 +33,118 @@ class ConvergerSpokeType(enum.Enum):
 
 
 class Spoke(SPCommunicator):
+    """Base spoke: the two channels and the length handshake."""
+
+    # payload length the spoke wants from the hub: "none" (bounds only) or
+    # "per_nonant" (one value per local nonant: W or nonants)
+    hub_payload = "none"
+
     def __init__(self, spbase_object, fullcomm, strata_comm, cylinder_comm, options=None):
         super().__init__(spbase_object, fullcomm, strata_comm, cylinder_comm, options)
-        self.local_write_id = 0
-        self.remote_write_id = 0
-        self.local_length = 0      # does NOT include the + 1
-        self.remote_length = 0     # length on the hub; does NOT include + 1
-        self.last_call_to_got_kill_signal = time.time()
+        self.to_hub = None
+        self.from_hub = None
+        self._hub_buf = None          # last buffer read from the hub (payload | outer, inner, id)
+        self._fresh = False           # the last poll brought a new buffer
 
-    def _make_windows(self, local_length, remote_length):
-        """spoke.py:34-58: tell the hub the two lengths, then build the windows."""
-        from .hub import _window_lengths
-        pairs = self.strata_comm.allgather_object((int(local_length), int(remote_length)))
-        self.local_length = local_length
-        self.remote_length = remote_length
-        spoke_lengths = [pairs[i + 1][0] for i in range(self.n_spokes)]
-        hub_lengths = [pairs[i + 1][1] for i in range(self.n_spokes)]
-        self._make_windows_from_lengths(_window_lengths(self.n_spokes, hub_lengths, spoke_lengths))
+    # ---- window setup: announce (own length, wanted length); the hub answers
+    #      with its own announcement (None) in the same all-gather
+    def _payload_length(self):
+        if self.hub_payload == "none":
+            return 0
+        scen = getattr(self.opt, "local_scenarios", None)
+        if scen is None:
+            raise RuntimeError("this spoke needs an opt object with local_scenarios")
+        if len(scen) == 0:
+            raise RuntimeError("Rank has zero local_scenarios")
+        return len(scen) * self.opt.batch.nonant.N
+
+    def make_windows(self):
+        mine = 1                                          # the bound
+        wanted = self._payload_length() + 2               # + outer, inner
+        ann = self.strata_comm.allgather_object((mine, wanted))
+        spokes = ann[1:]
+        self._make_windows_from_lengths(window_lengths([w for _, w in spokes], [m for m, _ in spokes]))
+        win = self.windows[self.strata_rank - 1]
+        self.to_hub = Outbox(win, self.strata_rank, mine, self.cylinder_comm)
+        self.from_hub = Inbox(win, 0, wanted, self.cylinder_comm)
+        self._hub_buf = np.zeros(wanted + 1)
+        self._bound_buf = np.zeros(mine + 1)
+
+    # ---- the reference's names for the two directions
+    @property
+    def local_write_id(self):
+        return self.to_hub.write_id if self.to_hub else 0
+
+    @property
+    def remote_write_id(self):
+        return self.from_hub.read_id if self.from_hub else 0
+
+    @property
+    def local_length(self):
+        return self.to_hub.length if self.to_hub else 0
+
+    @property
+    def remote_length(self):
+        return self.from_hub.length if self.from_hub else 0
 
     def spoke_to_hub(self, values):
-        """spoke.py:60-82."""
-        expected = self.local_length + 1
-        if len(values) != expected:
-            raise RuntimeError(f"Attempting to put array of length {len(values)} "
-                               f"into local buffer of length {expected}")
-        self.cylinder_comm.Barrier()
-        self.local_write_id += 1
-        values[-1] = self.local_write_id
-        self.windows[self.strata_rank - 1].put(values)
+        self.to_hub.publish(values)
 
     def spoke_from_hub(self, values):
-        """spoke.py:84-118."""
-        expected = self.remote_length + 1
-        if len(values) != expected:
-            raise RuntimeError(f"Spoke trying to get buffer of length {expected} "
-                               f"from hub, but provided buffer has length {len(values)}.")
-        self.cylinder_comm.Barrier()
-        self.windows[self.strata_rank - 1].get(0, values)
-        new_id = int(values[-1])
-        mm = self.cylinder_comm.allreduce_np(np.array([new_id, -new_id], dtype=np.int64), op="max")
-        max_id, min_id = int(mm[0]), -int(mm[1])
-        # only proceed if all the ranks agree on the id
-        if max_id != min_id:
-            return False
-        assert max_id == min_id == new_id
-        if new_id > self.remote_write_id or new_id < 0:
-            self.remote_write_id = new_id
-            return True
-        return False
+        return self.from_hub.poll(values)
 
     def got_kill_signal(self):
-        return self._got_kill_signal()
+        """Poll the hub's buffer once; True when it carries the kill signal."""
+        self._fresh = self.from_hub.poll(self._hub_buf)
+        return self.from_hub.killed
+
+    def get_serial_number(self):
+        """The write id of the last hub buffer accepted (its PH iteration tag)."""
+        return self.remote_write_id
 
     def main(self):
         raise NotImplementedError
 
-    def get_serial_number(self):
-        return self.remote_write_id
-
-    def _got_kill_signal(self):
-        raise NotImplementedError
-
 
 class _BoundSpoke(Spoke):
-    """spoke.py:147-208."""
+    """A spoke that sends one bound (optionally traced to a CSV file)."""
 
     def __init__(self, spbase_object, fullcomm, strata_comm, cylinder_comm, options=None):
         super().__init__(spbase_object, fullcomm, strata_comm, cylinder_comm, options)
-        tp = spbase_object.options.get("trace_prefix") if hasattr(spbase_object, "options") else None
-        if self.cylinder_rank == 0 and tp is not None:
-            filen = tp + self.__class__.__name__ + ".csv"
-            if os.path.exists(filen):
-                raise RuntimeError(f"Spoke trace file {filen} already exists!")
-            with open(filen, "w") as f:
+        self.trace_filen = None
+        opts = getattr(spbase_object, "options", None) or {}
+        prefix = opts.get("trace_prefix")
+        if prefix is not None and self.cylinder_rank == 0:
+            self.trace_filen = prefix + type(self).__name__ + ".csv"
+            if os.path.exists(self.trace_filen):
+                raise RuntimeError("spoke trace file %s exists already" % self.trace_filen)
+            with open(self.trace_filen, "w") as f:
                 f.write("time,bound\n")
-            self.trace_filen = filen
             self.start_time = spbase_object.start_time
-        else:
-            self.trace_filen = None
-        self._new_locals = False
-        self._bound = None
-        self._locals = None
-
-    def make_windows(self):
-        self._make_windows(1, 2)
-        self._locals = np.zeros(0 + 3)      # hub outer/inner bounds and kill signal
-        self._bound = np.zeros(1 + 1)       # spoke bound + write id
 
     @property
     def bound(self):
-        return self._bound[0]
+        return self._bound_buf[0]
 
     @bound.setter
     def bound(self, value):
-        self._append_trace(value)
-        self._bound[0] = value
-        self.spoke_to_hub(self._bound)
-
-    @property
-    def hub_inner_bound(self):
-        return self._locals[-2]
+        if self.trace_filen is not None:
+            with open(self.trace_filen, "a") as f:
+                f.write("%r,%r\n" % (time.perf_counter() - self.start_time, value))
+        self._bound_buf[0] = value
+        self.to_hub.publish(self._bound_buf)
 
     @property
     def hub_outer_bound(self):
-        return self._locals[-3]
+        return self._hub_buf[-3]
 
-    def _got_kill_signal(self):
-        self._new_locals = self.spoke_from_hub(self._locals)
-        return self.remote_write_id == -1
+    @property
+    def hub_inner_bound(self):
+        return self._hub_buf[-2]
 
-    def _append_trace(self, value):
-        if self.cylinder_rank != 0 or self.trace_filen is None:
-            return
-        with open(self.trace_filen, "a") as f:
-            f.write(f"{time.perf_counter() - self.start_time},{value}\n")
-
-
-class _BoundNonantLenSpoke(_BoundSpoke):
-    """spoke.py:211-236: the hub buffer holds one value per local nonant."""
-
-    def make_windows(self):
-        if not hasattr(self.opt, "local_scenarios"):
-            raise RuntimeError("Provided SPBase object does not have local_scenarios attribute")
-        if len(self.opt.local_scenarios) == 0:
-            raise RuntimeError("Rank has zero local_scenarios")
-        vbuflen = 2 + len(self.opt.local_scenarios) * self.opt.batch.nonant.N
-        self._make_windows(1, vbuflen)
-        self._locals = np.zeros(vbuflen + 1)
-        self._bound = np.zeros(1 + 1)
+    @property
+    def _payload(self):
+        return self._hub_buf[:-3]
 
 
 class InnerBoundSpoke(_BoundSpoke):
@@ -164,34 +157,36 @@ class OuterBoundSpoke(_BoundSpoke):
     converger_spoke_char = "O"
 
 
-class _BoundWSpoke(_BoundNonantLenSpoke):
+class OuterBoundWSpoke(_BoundSpoke):
+    """Receives W of every local scenario (scenario-major) with the bounds."""
+    converger_spoke_types = (ConvergerSpokeType.OUTER_BOUND, ConvergerSpokeType.W_GETTER)
+    converger_spoke_char = "O"
+    hub_payload = "per_nonant"
+
     @property
     def localWs(self):
-        return self._locals[:-3]
+        return self._payload
 
     @property
     def new_Ws(self):
-        return self._new_locals
+        return self._fresh
 
 
-class OuterBoundWSpoke(_BoundWSpoke):
-    converger_spoke_types = (ConvergerSpokeType.OUTER_BOUND, ConvergerSpokeType.W_GETTER)
-    converger_spoke_char = "O"
+class _NonantSpoke(_BoundSpoke):
+    hub_payload = "per_nonant"
 
-
-class _BoundNonantSpoke(_BoundNonantLenSpoke):
     @property
     def localnonants(self):
-        return self._locals[:-3]
+        return self._payload
 
     @property
     def new_nonants(self):
-        return self._new_locals
+        return self._fresh
 
 
-class InnerBoundNonantSpoke(_BoundNonantSpoke):
-    """spoke.py:306-363.  The best-solution cache keeps the device solution
-    (x of every local scenario) of the best incumbent."""
+class InnerBoundNonantSpoke(_NonantSpoke):
+    """Receives the hub's nonants, sends incumbents (inner bounds); keeps the
+    device solution of the best incumbent so finalize() can restore it."""
     converger_spoke_types = (ConvergerSpokeType.INNER_BOUND, ConvergerSpokeType.NONANT_GETTER)
     converger_spoke_char = "I"
 
@@ -202,16 +197,18 @@ class InnerBoundNonantSpoke(_BoundNonantSpoke):
         self.solver_options = None
         self.best_solution_cache = None
 
+    def _better(self, value):
+        return value < self.best_inner_bound if self.is_minimizing else value > self.best_inner_bound
+
     def update_if_improving(self, candidate_inner_bound):
-        if candidate_inner_bound is None:
-            return False
-        update = (candidate_inner_bound < self.best_inner_bound) if self.is_minimizing \
-            else (self.best_inner_bound < candidate_inner_bound)
-        if not update:
+        """Send the candidate if it improves on the best so far (and cache the
+        solution that produced it); returns whether it did."""
+        if candidate_inner_bound is None or not self._better(candidate_inner_bound):
             return False
         self.best_inner_bound = candidate_inner_bound
         self.bound = candidate_inner_bound
-        self._cache_best_solution()
+        self.opt._settle()
+        self.best_solution_cache = self.opt._x.clone()
         return True
 
     def finalize(self):
@@ -225,11 +222,7 @@ class InnerBoundNonantSpoke(_BoundNonantSpoke):
         self.final_bound = self.bound
         return self.final_bound
 
-    def _cache_best_solution(self):
-        self.opt._settle()
-        self.best_solution_cache = self.opt._x.clone()
 
-
-class OuterBoundNonantSpoke(_BoundNonantSpoke):
+class OuterBoundNonantSpoke(_NonantSpoke):
     converger_spoke_types = (ConvergerSpokeType.OUTER_BOUND, ConvergerSpokeType.NONANT_GETTER)
     converger_spoke_char = "A"
