@@ -197,3 +197,85 @@ def nonant_spec_from_models(names, models):
         if cols != slot_col:
             raise RuntimeError("scenario %s: nonant columns differ from scenario %s" % (names[k], names[0]))
     return NonantSpec(slot_col, slot_stage, slot_local, node_names, cond_prob, vnames)
+
+
+def bundle_batch(b, groups, probs):
+    """The EF bundles of a two-stage batch as one batch whose "scenarios" are
+    the bundles (``SPOpt.subproblem_creation`` + ``FormEF``, spopt.py:743-836).
+
+    groups[g]: local scenario indices of bundle g; probs: (S,) scenario
+    probabilities.  Every bundle gets K = max group size member blocks (a
+    smaller bundle repeats its first scenario with weight 0: the same rows on
+    the same nonants, no cost -- the feasible nonants and the optimum are
+    unchanged, and every bundle shares one sparsity pattern).  Column layout:
+    [the N shared nonant columns | member 0's other columns | member 1's | ...];
+    the nonant columns are shared (the EF's nonanticipativity equalities
+    substituted out), their bounds the members' intersection.  Costs are
+    weighted by p_s / p_bundle (the EF objective's normalisation,
+    sputils.py:273-275), so the PH terms of the bundle lane are the weighted
+    sums of its members' (SPOpt.solve_loop aggregates W and rho the same way).
+
+    Returns (BatchData of the bundles, member index array (G, K), weights (G, K),
+    column map (K, n): bundle column of each member column)."""
+    nn = b.nonant
+    if nn.nstages > 1:
+        raise NotImplementedError("bundles of multistage trees (nonants below ROOT) are not supported")
+    S, n, m, N = b.S, b.n, b.m, nn.N
+    G = len(groups)
+    K = max(len(g) for g in groups)
+    members = np.array([list(g) + [g[0]] * (K - len(g)) for g in groups], dtype=np.int64)
+    p = np.asarray(probs, dtype=np.float64)
+    pB = np.array([sum(p[s] for s in g) for g in groups])
+    wts = np.array([[p[s] / pB[gi] if r < len(g) else 0.0 for r, s in enumerate(members[gi])]
+                    for gi, g in enumerate(groups)])
+    slot_of = {int(c): t for t, c in enumerate(nn.slot_col)}
+    others = [j for j in range(n) if j not in slot_of]
+    no = len(others)
+    colmap = np.zeros((K, n), dtype=np.int64)
+    for r in range(K):
+        for j in range(n):
+            colmap[r, j] = slot_of[j] if j in slot_of else N + r * no + others.index(j)
+    nB = N + K * no
+    # rows: member r's rows, columns mapped and sorted within the row
+    rowptr, colidx, src = [0], [], []          # src: (member, original nnz index) per bundle entry
+    for r in range(K):
+        for i in range(m):
+            ks = list(range(b.rowptr[i], b.rowptr[i + 1]))
+            ks.sort(key=lambda k: colmap[r, b.colidx[k]])
+            for k in ks:
+                colidx.append(int(colmap[r, b.colidx[k]]))
+                src.append((r, k))
+            rowptr.append(len(colidx))
+    A = np.zeros((G, len(src)))
+    for e, (r, k) in enumerate(src):
+        A[:, e] = b.A_full[members[:, r], k]
+
+    def per(a, width):
+        a = np.asarray(a, dtype=np.float64)
+        return a if a.ndim == 2 else np.broadcast_to(a, (S, width))
+
+    c, lb, ub = per(b.c, n), per(b.lb, n), per(b.ub, n)
+    bl, bu = per(b.bl, m), per(b.bu, m)
+    cB = np.zeros((G, nB))
+    lbB = np.zeros((G, nB))
+    ubB = np.zeros((G, nB))
+    lbB[:, :N], ubB[:, :N] = -np.inf, np.inf
+    for r in range(K):
+        sr = members[:, r]
+        for j in range(n):
+            q = colmap[r, j]
+            cB[:, q] += wts[:, r] * c[sr, j]
+            if q < N:
+                lbB[:, q] = np.maximum(lbB[:, q], lb[sr, j])
+                ubB[:, q] = np.minimum(ubB[:, q], ub[sr, j])
+            else:
+                lbB[:, q], ubB[:, q] = lb[sr, j], ub[sr, j]
+    blB = np.concatenate([bl[members[:, r]] for r in range(K)], axis=1)
+    buB = np.concatenate([bu[members[:, r]] for r in range(K)], axis=1)
+    c0B = (wts * b.c0[members]).sum(axis=1)
+    names = ["bundle%d" % g for g in range(G)]
+    vn = [b.var_names[j] if b.var_names else "x%d" % j for j in nn.slot_col]
+    spec = NonantSpec(np.arange(N), np.ones(N, dtype=np.int32), nn.slot_local, [None], [np.ones(G)], nn.var_names)
+    out = BatchData(names, rowptr, colidx, A, blB, buB, lbB, ubB, cB, c0B, b.sense, pB, spec,
+                    var_names=vn + ["b%d" % q for q in range(N, nB)])
+    return out, members, wts, colmap

@@ -478,6 +478,8 @@ class PHBase(SPOpt):
             return False
         if o["display_progress"] or o["verbose"] or o["display_convergence_detail"]:
             return False
+        if self._bundles is not None:           # (the bundles' solve is host-driven)
+            return False
         so = self.current_solver_options or {}
         if not int(so.get("native_loop", 1)):
             return False

@@ -80,9 +80,10 @@ class SPBase:
         if self.n_proc > len(self.all_scenario_names):
             raise RuntimeError("More ranks than scenarios")
         self._calculate_scenario_ranks()
-        if "bundles_per_rank" in self.options and self.options["bundles_per_rank"] > 0:
-            raise NotImplementedError("bundles (EF subproblems) are not supported by the batched engine")
-        self.bundling = False
+        # EF bundles (spbase.py:219-253): bundles_per_rank slices of each rank's scenarios
+        self.bundling = int(self.options.get("bundles_per_rank", 0) or 0) > 0
+        if self.bundling and self.n_proc * int(self.options["bundles_per_rank"]) > len(self.all_scenario_names):
+            raise RuntimeError("Not enough scenarios to satisfy the bundles_per_rank requirement")
         self._native = _native_lib if _native_lib is not None else _native.load()
         if _device is None:
             if not torch.cuda.is_available():
@@ -98,9 +99,22 @@ class SPBase:
         self._use_variable_probability_setter()
         self._create_communicators()
         self._upload_batch()
+        self._bundles = None
+        if self.bundling:
+            self._setup_bundles()
         self._spcomm = None
         self.tree_solution_available = False
         self.first_stage_solution_available = False
+
+    def _setup_bundles(self):
+        """The bundles of this rank (names_in_bundles as the reference holds it:
+        {rank: {bundle: [scenario names]}}) and their device solver."""
+        from .bundles import BundleSolver, assign_bundles
+        B = int(self.options["bundles_per_rank"])
+        groups = assign_bundles(len(self.local_scenario_names), B)
+        self.names_in_bundles = {self.cylinder_rank: {g: [self.local_scenario_names[k] for k in grp]
+                                                      for g, grp in enumerate(groups)}}
+        self._bundles = BundleSolver(self, groups)
 
     # ------------------------------------------------------------ tree/ranks
     def _check_nodenames(self):

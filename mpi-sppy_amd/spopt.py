@@ -186,16 +186,20 @@ class SPOpt(SPBase):
         # enqueued and the next PH step's reductions queue behind them; every
         # reader of solve results calls _settle() (convergence_diff finishes it
         # and redoes the step in the rare case a scenario needed the generic path).
-        defer = (self.extensions is None and not dtiming and so.lane_solver
+        defer = (self.extensions is None and not dtiming and so.lane_solver and self._bundles is None
                  and bool((solver_options or {}).get("defer", 1)))
         so.defer = 1 if defer else 0
         self._set_ph_terms()
         total = ctypes.c_int32(0)
         t0 = time.perf_counter()
         self._x_touched = True
-        lib.check(self._ctx, lib.solve(self._ctx, ctypes.byref(so), self._x.data_ptr(), self._y.data_ptr(),
-                                       self._obj.data_ptr(), self._status.data_ptr(), self._iters.data_ptr(),
-                                       ctypes.byref(total), self._stream()), "solve")
+        if self._bundles is not None:
+            # EF bundles: one batched solve of the bundles, scenario results from it
+            total.value = self._bundles.solve(so)
+        else:
+            lib.check(self._ctx, lib.solve(self._ctx, ctypes.byref(so), self._x.data_ptr(), self._y.data_ptr(),
+                                           self._obj.data_ptr(), self._status.data_ptr(), self._iters.data_ptr(),
+                                           ctypes.byref(total), self._stream()), "solve")
         self._conv_cache = None
         self._bump()
         if getattr(self, "_fix_lb", None) is not None:
@@ -228,7 +232,8 @@ class SPOpt(SPBase):
     def _record_solve(self, rec, total, stragglers):
         lib = self._native
         stt = _native.SolveStats()
-        lib.check(self._ctx, lib.last_solve_stats(self._ctx, ctypes.byref(stt)), "last_solve_stats")
+        ctx = self._ctx if self._bundles is None else self._bundles.ctx
+        lib.check(ctx, lib.last_solve_stats(ctx, ctypes.byref(stt)), "last_solve_stats")
         n_bad = int(stt.not_optimal) + int(stt.infeasible)
         t0, gripe = rec.pop("t0"), rec.pop("gripe")
         rec.update({"pdhg_iters": total, "pdhg_ms": stt.pdhg_ms, "launches": stt.pdhg_launches,
@@ -610,6 +615,8 @@ class SPOpt(SPBase):
             lib.check(self._ctx, lib.set_bounds(self._ctx, None, None, self._stream()), "set_bounds")
             self._fix_lb = self._fix_ub = None
         else:
+            if self._bundles is not None:
+                raise NotImplementedError("fixing nonants of bundled scenarios (bundles_per_rank) is not supported")
             b = self.batch
             n, S = b.n, self._S
             cols = torch.as_tensor(b.nonant.slot_col.astype(np.int64), device=self.device)

@@ -242,3 +242,75 @@ def evaluate_xhat(scens, cache, stage_max=None):
         objs[k] = float(np.dot(s.c, x)) + s.c0 if ok else np.nan
     E = math.fsum(s.prob * o for s, o in zip(scens, objs))
     return E, objs, feas
+
+
+def assign_bundles(S, n_proc, bundles_per_rank):
+    """``SPBase._assign_bundles`` (spbase.py:219-253) restated: per rank, its
+    contiguous scenario slice cut into bundles_per_rank slices range(int(i *
+    avg), int((i + 1) * avg)), avg = count / bundles_per_rank."""
+    out = []
+    for sl in rank_slices(S, n_proc):
+        avg = len(sl) / bundles_per_rank
+        out += [[sl[i] for i in range(int(b * avg), int((b + 1) * avg))] for b in range(bundles_per_rank)]
+    return out
+
+
+class OracleBundledPH(OraclePH):
+    """PH with EF bundles (``bundles_per_rank``): each bundle's subproblem is the
+    extensive form of its scenarios as ``SPOpt.FormEF`` builds it
+    (spopt.py:743-836, sputils.py:241-341): every scenario keeps its own
+    variables, nonanticipativity equalities x_s[slot] == x_first[slot] per tree
+    node, and the objective sum_s p_s (f_s + W_s x_s + rho/2 |x_s - xbar|^2) /
+    p_bundle (normalised, sputils.py:273-275).  x-bar, W and the convergence
+    metric stay per scenario (phbase.py:27-107, 293-343)."""
+
+    def __init__(self, scens, bundles, rho=1.0, n_proc=1, sense=1):
+        super().__init__(scens, rho=rho, n_proc=n_proc, sense=sense)
+        self.bundles = [list(b) for b in bundles]
+
+    def _bundle_qp(self, members):
+        import scipy.sparse as sp
+        pB = sum(self.scens[k].prob for k in members)
+        qs, ps, As, bls, bus, lbs, ubs = [], [], [], [], [], [], []
+        for k in members:
+            q, p = self._qp_data(k)
+            w = self.scens[k].prob / pB
+            qs.append(w * q)
+            ps.append(w * p)
+            s = self.scens[k]
+            As.append(s.A)
+            bls.append(s.bl)
+            bus.append(s.bu)
+            lbs.append(s.lb)
+            ubs.append(s.ub)
+        ns = [len(self.scens[k].c) for k in members]
+        off = np.concatenate([[0], np.cumsum(ns)])
+        n = int(off[-1])
+        A = sp.block_diag(As).toarray()
+        bl, bu = np.concatenate(bls), np.concatenate(bus)
+        first, extra = {}, []
+        for b, k in enumerate(members):
+            for j in range(self.N):
+                key = (self.node_of[k][j], j)
+                col = off[b] + self.ncol[k, j]
+                if key not in first:
+                    first[key] = col
+                else:
+                    r = np.zeros(n)
+                    r[col], r[first[key]] = 1.0, -1.0
+                    extra.append(r)
+        if extra:
+            A = np.vstack([A, np.array(extra)])
+            bl = np.concatenate([bl, np.zeros(len(extra))])
+            bu = np.concatenate([bu, np.zeros(len(extra))])
+        return (A, bl, bu, np.concatenate(lbs), np.concatenate(ubs), np.concatenate(qs), np.concatenate(ps)), off
+
+    def solve_loop(self):
+        for members in self.bundles:
+            (A, bl, bu, lb, ub, q, p), off = self._bundle_qp(members)
+            x, feas = qp.solve(A, bl, bu, lb, ub, q, p)
+            if not feas:
+                raise RuntimeError("oracle: infeasible bundle %s" % members)
+            for b, k in enumerate(members):
+                self.x[k] = x[off[b]:off[b + 1]].copy()
+                self.obj[k] = self.scen_objective(k, self.x[k])
