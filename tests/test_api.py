@@ -34,10 +34,11 @@ def test_root_required(emu):
         PH(ph_options(1), ["scen0"], farmer.scenario_creator, all_nodenames=["A"], _native_lib=emu, _device="cpu")
 
 
-def test_bundles_rejected(emu):
+def test_bundles_need_scenarios(emu):
+    """spbase.py:232-235: more bundles than scenarios is an error."""
     opts = ph_options(1)
-    opts["bundles_per_rank"] = 2
-    with pytest.raises(NotImplementedError):
+    opts["bundles_per_rank"] = 3
+    with pytest.raises(RuntimeError, match="bundles_per_rank"):
         PH(opts, ["scen0", "scen1"], farmer.scenario_creator, _native_lib=emu, _device="cpu")
 
 
