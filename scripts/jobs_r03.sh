@@ -36,5 +36,8 @@ case "$1" in
           "bench:r03_s12_c5b:--only C5b $A" ;;
   s13) PHX_WG_PROF=1 $J "bench:r03_s13_c2_wgprof:--only C2 $A --so {\"native_loop\":0}" && \
        PHX_SP_GRID=64 $J "bench:r03_s13_c5b_g64:--only C5b $A" && PHX_SP_GRID=128 $J "bench:r03_s13_c5b_g128:--only C5b $A" ;;
+  s14) $J "test:tests" "bench:r03_s14_bench:$H" "trace:r03_s14_trace:$H --ar-probe 0" && \
+       PHX_WG_PROF=1 $J "bench:r03_s13_c2_wgprof:--only C2 $A --so {\"native_loop\":0}" && \
+       PHX_SP_GRID=64 $J "bench:r03_s13_c5b_g64:--only C5b $A" && PHX_SP_GRID=128 $J "bench:r03_s13_c5b_g128:--only C5b $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
