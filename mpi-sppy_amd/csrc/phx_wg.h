@@ -139,6 +139,30 @@ PHX_HD double wg_max(double v, double* red) {
     return v;
 }
 
+// max of two values over the workgroup in one LDS round (two barriers)
+PHX_HD void wg_max2(double& a, double& b, double* red) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    for (int o = 32; o > 0; o >>= 1) {
+        a = fmax(a, __shfl_xor(a, o, 64));
+        b = fmax(b, __shfl_xor(b, o, 64));
+    }
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) {
+        red[threadIdx.x >> 6] = a;
+        red[4 + (threadIdx.x >> 6)] = b;
+    }
+    __syncthreads();
+    a = red[0];
+    b = red[4];
+    for (int w = 1; w < WG_NT / 64; ++w) {
+        a = fmax(a, red[w]);
+        b = fmax(b, red[4 + w]);
+    }
+#else
+    (void)a; (void)b; (void)red;
+#endif
+}
+
 // sum of a value over a quad (its four threads end with the same sum)
 PHX_HD double wg_quad_sum(double v) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -442,8 +466,8 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
                 L.z[i] = zn;
             }
             // stop once the correction vanishes (phx_lane.h kkt_refine's rule)
-            const double dmx = wg_max(dmax, L.red);
-            const bool done = dmx <= 1e-10 * (1.0 + wg_max(xmax, L.red));
+            wg_max2(dmax, xmax, L.red);
+            const bool done = dmax <= 1e-10 * (1.0 + xmax);
             WG_CNT(8);
             if (done) break;
         }
