@@ -39,5 +39,11 @@ case "$1" in
   s14) $J "test:tests" "bench:r03_s14_bench:$H" "trace:r03_s14_trace:$H --ar-probe 0" && \
        PHX_WG_PROF=1 $J "bench:r03_s13_c2_wgprof:--only C2 $A --so {\"native_loop\":0}" && \
        PHX_SP_GRID=64 $J "bench:r03_s13_c5b_g64:--only C5b $A" && PHX_SP_GRID=128 $J "bench:r03_s13_c5b_g128:--only C5b $A" ;;
+  s15) $J "test:tests" "bench:r03_s15_bench_default:" "prof:r03_s15_prof:$B" \
+          "pmc:r03_s15_pmc_fetch:FETCH_SIZE:$B" "pmc:r03_s15_pmc_write:WRITE_SIZE:$B" "pmc:r03_s15_pmc_sq:$SQ:$B" ;;
+  s16) $J "pmc:r03_s16_pmc1m_fetch:FETCH_SIZE:$M" "pmc:r03_s16_pmc1m_write:WRITE_SIZE:$M" \
+          "pmc:r03_s16_c2_fetch:FETCH_SIZE:--only C2 $A" "pmc:r03_s16_c2_write:WRITE_SIZE:--only C2 $A" \
+          "pmc:r03_s16_c5a_fetch:FETCH_SIZE:--only C5a $A" "pmc:r03_s16_c5a_write:WRITE_SIZE:--only C5a $A" \
+          "pmc:r03_s16_c5b_fetch:FETCH_SIZE:--only C5b $A" "pmc:r03_s16_c5b_write:WRITE_SIZE:--only C5b $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
