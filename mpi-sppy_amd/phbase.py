@@ -364,7 +364,7 @@ class PHBase(SPOpt):
         if device_sums:
             self._expect_key = None
             if self.n_proc == 1:
-                self._iter0_checks(self._iter0_exp_host.numpy().copy())
+                self._iter0_checks(self._iter0_exp_host.tolist())
             else:
                 self._iter0_checks(self._sums_over_ranks(self._expect_buf))
             return
