@@ -118,6 +118,11 @@ typedef struct phx_solve_opts {
                                  of the rescue pass before any interior point,
                                  and of the first warm pass after a cold solve;
                                  0: max(16, 8 as_rounds)                      */
+    double  lane_ipm_tol;     /* lane solver's interior point: relative KKT
+                                 error at which it stops -- it only has to
+                                 expose the active set (classification, then
+                                 active-set rounds certify to kkt_tol);
+                                 0: ipm_tol                                   */
 } phx_solve_opts;
 
 /* Statistics of the most recent phx_solve (HIP events on the solve stream). */

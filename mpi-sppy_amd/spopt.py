@@ -14,7 +14,7 @@ phbase.py:273-275): keys ``pdhg_max_iters``, ``pdhg_check_every``,
 ``pdhg_restart_max``, ``polish``, ``polish_refine``, ``polish_below``,
 ``kkt_tol``, ``opt_tol``, ``polish_reg``, ``warm_start``, ``ipm_after``,
 ``ipm_max_it``, ``ipm_tol``, ``lane_solver``, ``as_rounds``, ``warm_passes``, ``wg_warm``,
-``sp``, ``sp_rounds``, ``seed_templates``, ``rescue_rounds``.
+``sp``, ``sp_rounds``, ``seed_templates``, ``rescue_rounds``, ``lane_ipm_tol``.
 """
 import ctypes
 import inspect
@@ -49,6 +49,7 @@ SOLVER_DEFAULTS = {
     "sp_rounds": 16,
     "seed_templates": 64,
     "rescue_rounds": 0,
+    "lane_ipm_tol": 0.0,
 }
 
 OPTIMAL, ITER_LIMIT, NUMERIC_FAIL, INFEASIBLE = 1, 2, 3, 4
@@ -156,6 +157,7 @@ class SPOpt(SPBase):
         so.sp_rounds = int(o["sp_rounds"])
         so.seed_templates = int(o["seed_templates"])
         so.rescue_rounds = int(o["rescue_rounds"])
+        so.lane_ipm_tol = float(o["lane_ipm_tol"])
         return so
 
     def _set_ph_terms(self):

@@ -29,7 +29,7 @@ for step in "$@"; do
     prof)
       tag="${rest%%:*}"; args="${rest#*:}"; log="gpurun_out/${tag}.log"
       echo "== step $n: rocprofv3 --kernel-trace --stats bench.py $args"
-      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "gpurun_out/${tag}" -o run -- python3 bench.py $args > "$log" 2>&1
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "gpurun_out/${tag}" -o run -- python3 bench.py $args > "$log" 2>&1
       rc=$?; tail -2 "$log" ;;
     trace)
       tag="${rest%%:*}"; args="${rest#*:}"; log="gpurun_out/${tag}.log"

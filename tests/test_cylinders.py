@@ -38,7 +38,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, out):
+def _worker(rank, world, port, out, gpu=False):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
@@ -53,7 +53,10 @@ def _worker(rank, world, port, out):
     from mpisppy_amd.phbase import PHBase
     from mpisppy_amd.spin_the_wheel import WheelSpinner
     from helpers import ph_options
-    emu = _native.Lib(os.path.join(ROOT, "tests", "emu", "libphx_emu.so"), prefix="emu_phx_")
+    if gpu:     # the product library on cuda:0 (both cylinders share the one GPU)
+        lib, device = _native.load(), "cuda:0"
+    else:
+        lib, device = _native.Lib(os.path.join(ROOT, "tests", "emu", "libphx_emu.so"), prefix="emu_phx_"), "cpu"
     names = farmer.scenario_names_creator(S)
 
     sent = []       # the hub's W per write id
@@ -71,7 +74,7 @@ def _worker(rank, world, port, out):
             return b
 
     okw = dict(options=ph_options(ITERS), all_scenario_names=names, scenario_creator=farmer.scenario_creator,
-               scenario_creator_kwargs={"num_scens": S}, _native_lib=emu, _device="cpu")
+               scenario_creator_kwargs={"num_scens": S}, _native_lib=lib, _device=device)
     hub_dict = {"hub_class": RecordingHub, "hub_kwargs": {"options": {"display_progress": False}},
                 "opt_class": PH, "opt_kwargs": dict(okw)}
     spoke_dict = {"spoke_class": RecordingSpoke, "opt_class": PHBase, "opt_kwargs": dict(okw)}
@@ -93,10 +96,10 @@ def _worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
-def _run(world):
+def _run(world, gpu=False):
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), out, gpu), nprocs=world, join=True)
     return [out[r] for r in range(world)]
 
 
@@ -110,7 +113,7 @@ def _oracle_lagrangian(W_flat):
     return o.Ebound()
 
 
-def _check(res, ncyl):
+def _check(res, ncyl, tol=1e-9):
     from oracle import models as om, ph as oph
     hubs = [r for r in res if r["strata_rank"] == 0]
     spokes = [r for r in res if r["strata_rank"] == 1]
@@ -147,7 +150,7 @@ def _check(res, ncyl):
             continue
         assert np.array_equal(Wloc, W_by_id[wid]), wid
         ob = _oracle_lagrangian(W_by_id[wid])
-        assert b == pytest.approx(ob, rel=1e-9, abs=1e-7), (wid, b, ob)
+        assert b == pytest.approx(ob, rel=tol, abs=1e-7), (wid, b, ob)
         bounds.append(b)
     # the spoke's first bound is the trivial bound (W = 0, serial number 0)
     assert g0[0][0] == 0 and g0[0][1] == pytest.approx(h0["trivial"], rel=1e-12)
@@ -164,6 +167,14 @@ def _check(res, ncyl):
 
 def test_wheel_lagrangian_1x(emu):
     _check(_run(2), 1)
+
+
+@pytest.mark.gpu
+def test_wheel_lagrangian_gpu():
+    """The same wheel (hub + Lagrangian spoke, two processes over gloo and the
+    shared-memory windows) on the real kernels: both cylinders' contexts on
+    cuda:0; every bound the spoke sent equals the oracle's for the W it read."""
+    _check(_run(2, gpu=True), 1, tol=1e-8)
 
 
 def test_wheel_lagrangian_2x(emu):
