@@ -97,11 +97,16 @@ class BatchData:
             return a[0].copy(), False
         return a, True
 
-    def compress(self):
-        """Split invariant / varying parts (exact equality, NaN-free data)."""
+    def compress(self, force_var=None, force_rhs_vary=False):
+        """Split invariant / varying parts (exact equality, NaN-free data).
+        force_var: A entries kept varying even where equal now (a structure
+        that must not change when they do); force_rhs_vary: row bounds per
+        scenario."""
         S = self.S
         A = self.A_full
         same = np.all(A == A[0:1], axis=0) if S > 1 else np.ones(self.nnz, bool)
+        if force_var is not None:
+            same = same & ~np.asarray(force_var, dtype=bool)
         self.kvar = np.full(self.nnz, -1, dtype=np.int32)
         var_k = np.nonzero(~same)[0]
         self.kvar[var_k] = np.arange(len(var_k), dtype=np.int32)
@@ -119,7 +124,7 @@ class BatchData:
             self.lb, self.ub, self.bnd_vary = lb, ub, False
         bl, blv = self._squeeze(self.bl, S)
         bu, buv = self._squeeze(self.bu, S)
-        if blv or buv:
+        if blv or buv or force_rhs_vary:
             self.bl = np.broadcast_to(self.bl, (S, self.m)).copy() if self.bl.ndim == 1 else self.bl
             self.bu = np.broadcast_to(self.bu, (S, self.m)).copy() if self.bu.ndim == 1 else self.bu
             self.rhs_vary = True

@@ -84,11 +84,16 @@ class PHBase(SPOpt):
 
     def attach_PH_to_objective(self, add_duals, add_prox):
         """The PH terms are applied by the native solver (phx_set_ph_terms);
-        linearised prox (phbase.py:628-692) is not supported."""
-        if self.options.get("linearize_proximal_terms", False):
-            raise NotImplementedError("linearize_proximal_terms is not supported by the batched engine")
+        with ``linearize_proximal_terms`` the prox term's x^2 is replaced by
+        tangent cuts (phbase.py:628-692; prox_approx.py)."""
         self._attach_duals = bool(add_duals)
         self._attach_prox = bool(add_prox)
+        if add_prox and self.options.get("linearize_proximal_terms", False) and self.batch.nonant.N:
+            from .prox_approx import ProxLinSolver
+            if self._bundles is not None:
+                raise NotImplementedError("linearize_proximal_terms with bundles_per_rank is not supported")
+            self._prox_lin = ProxLinSolver(self, self.options.get("proximal_linearization_tolerance", 1.e-1),
+                                           self.options.get("initial_proximal_cut_count", 2))
 
     def PH_Prep(self, attach_duals=True, attach_prox=True):
         self.attach_Ws_and_prox()
@@ -478,7 +483,7 @@ class PHBase(SPOpt):
             return False
         if o["display_progress"] or o["verbose"] or o["display_convergence_detail"]:
             return False
-        if self._bundles is not None:           # (the bundles' solve is host-driven)
+        if self._bundles is not None or self._prox_lin is not None:   # (host-driven solves)
             return False
         so = self.current_solver_options or {}
         if not int(so.get("native_loop", 1)):

@@ -100,6 +100,7 @@ class SPBase:
         self._create_communicators()
         self._upload_batch()
         self._bundles = None
+        self._prox_lin = None          # linearised prox terms (prox_approx.ProxLinSolver), PHBase sets it
         if self.bundling:
             self._setup_bundles()
         self._spcomm = None

@@ -189,19 +189,27 @@ class SPOpt(SPBase):
         # reader of solve results calls _settle() (convergence_diff finishes it
         # and redoes the step in the rare case a scenario needed the generic path).
         defer = (self.extensions is None and not dtiming and so.lane_solver and self._bundles is None
-                 and bool((solver_options or {}).get("defer", 1)))
+                 and self._prox_lin is None and bool((solver_options or {}).get("defer", 1)))
         so.defer = 1 if defer else 0
         self._set_ph_terms()
         total = ctypes.c_int32(0)
         t0 = time.perf_counter()
         self._x_touched = True
+        self._solve_ctx = self._ctx
         if self._bundles is not None:
             # EF bundles: one batched solve of the bundles, scenario results from it
             total.value = self._bundles.solve(so)
+            self._solve_ctx = self._bundles.ctx
+        elif self._prox_lin is not None and self.prox_on and self.batch.nonant.N:
+            # linearised prox: the LP with the tangent cuts, in its own context
+            total.value = self._prox_lin.solve(so)
+            self._solve_ctx = self._prox_lin.ctx
         else:
             lib.check(self._ctx, lib.solve(self._ctx, ctypes.byref(so), self._x.data_ptr(), self._y.data_ptr(),
                                            self._obj.data_ptr(), self._status.data_ptr(), self._iters.data_ptr(),
                                            ctypes.byref(total), self._stream()), "solve")
+            if self._prox_lin is not None:
+                self._prox_lin.after_plain_solve()
         self._conv_cache = None
         self._bump()
         if getattr(self, "_fix_lb", None) is not None:
@@ -234,7 +242,7 @@ class SPOpt(SPBase):
     def _record_solve(self, rec, total, stragglers):
         lib = self._native
         stt = _native.SolveStats()
-        ctx = self._ctx if self._bundles is None else self._bundles.ctx
+        ctx = getattr(self, "_solve_ctx", None) or self._ctx
         lib.check(ctx, lib.last_solve_stats(ctx, ctypes.byref(stt)), "last_solve_stats")
         n_bad = int(stt.not_optimal) + int(stt.infeasible)
         t0, gripe = rec.pop("t0"), rec.pop("gripe")
@@ -315,6 +323,10 @@ class SPOpt(SPBase):
         self._settle()
         if not hasattr(self, "_obj_eval"):
             self._obj_eval = torch.zeros_like(self._obj)
+        if self._prox_lin is not None:
+            self._prox_lin.objective_into(self._obj_eval)
+            self._bump()
+            return
         self._set_ph_terms()
         lib = self._native
         lib.check(self._ctx, lib.objective(self._ctx, self._x.data_ptr(), self._obj_eval.data_ptr(),

@@ -314,3 +314,112 @@ class OracleBundledPH(OraclePH):
             for b, k in enumerate(members):
                 self.x[k] = x[off[b]:off[b + 1]].copy()
                 self.obj[k] = self.scen_objective(k, self.x[k])
+
+
+def _prox_initial_points(lb, ub, count):
+    """``ProxApproxManagerContinuous._create_initial_cuts`` (utils/prox_approx.py:124-141)."""
+    pts = []
+    if lb != 0.0:
+        pts.append(float(lb))
+    if lb == ub:
+        return pts
+    if ub != 0.0:
+        pts.append(float(ub))
+    if count > 2:
+        delta = (ub - lb) / (count - 1)
+        pts += [lb + i * delta for i in range(1, count - 1)]
+    return pts
+
+
+def _prox_newton(x_pnt, y_pnt):
+    """``check_tol_add_cut``'s projection loop (utils/prox_approx.py:95-115)."""
+    def step(v):
+        return v - (v * (1 - 2 * y_pnt + 2 * v * v) - x_pnt) / (1 + 6 * v * v - 2 * y_pnt)
+    this_val = x_pnt
+    next_val = step(this_val)
+    while not math.isclose(this_val, next_val, rel_tol=1e-6, abs_tol=1e-6):
+        this_val = next_val
+        next_val = step(this_val)
+    return next_val
+
+
+class OracleLinProxPH(OraclePH):
+    """PH with ``linearize_proximal_terms`` (phbase.py:570-582, 617-699;
+    utils/prox_approx.py): per scenario and nonant a variable xsq >= 0 with
+    tangent cuts xsq >= 2 a x - a^2; the prox term is rho/2 (xsq - 2 xbar x +
+    xbar^2), so prox-on subproblems are LPs.  Before each prox-on solve every
+    nonant whose last (x, xsq) has x^2 - xsq > tol gets a cut at the Newton
+    projection of that point onto y = x^2.  Prox-off solves are the plain LPs
+    (xsq has zero cost there); xsq then takes its least feasible value
+    max(0, max_k tangent_k(x)), the value of a simplex basis."""
+
+    def __init__(self, scens, rho=1.0, tol=0.1, initial_cuts=2, n_proc=1, sense=1):
+        super().__init__(scens, rho=rho, n_proc=n_proc, sense=sense)
+        self.tol = tol
+        self.cuts = []
+        for k, s in enumerate(scens):
+            row = []
+            for j in range(self.N):
+                col = self.ncol[k, j]
+                lb, ub = float(s.lb[col]), float(s.ub[col])
+                if not (math.isfinite(lb) and math.isfinite(ub)):
+                    raise RuntimeError("linearize_nonbinary_proximal_terms requires bounded nonants")
+                row.append(_prox_initial_points(lb, ub, initial_cuts))
+            self.cuts.append(row)
+        self.xsq = np.zeros((self.S, self.N))
+
+    def _envelope(self, k, xn):
+        return np.array([max([0.0] + [2 * a * xn[j] - a * a for a in self.cuts[k][j]]) for j in range(self.N)])
+
+    def update_prox_approx(self):
+        for k in range(self.S):
+            xn = self.x[k][self.ncol[k]]
+            for j in range(self.N):
+                if xn[j] ** 2 - self.xsq[k, j] > self.tol:
+                    self.cuts[k][j].append(_prox_newton(float(xn[j]), float(self.xsq[k, j])))
+
+    def solve_loop(self):
+        if not self.prox_on:
+            super().solve_loop()
+            for k in range(self.S):
+                self.xsq[k] = self._envelope(k, self.x[k][self.ncol[k]])
+            return
+        if self.x[0] is not None:
+            self.update_prox_approx()
+        for k, s in enumerate(self.scens):
+            n, N = len(s.c), self.N
+            q = np.concatenate([s.c, 0.5 * self.rho[k]])
+            cols = self.ncol[k]
+            if self.W_on:
+                q[cols] += self.W[k]
+            q[cols] -= self.rho[k] * self.xbar[k]
+            rows, bl, bu = [], [], []
+            for j in range(N):
+                for a in self.cuts[k][j]:
+                    r = np.zeros(n + N)
+                    r[cols[j]], r[n + j] = -2.0 * a, 1.0
+                    rows.append(r)
+                    bl.append(-a * a)
+                    bu.append(np.inf)
+            A = np.hstack([np.asarray(s.A.todense() if hasattr(s.A, "todense") else s.A), np.zeros((s.A.shape[0], N))])
+            if rows:
+                A = np.vstack([A, np.array(rows)])
+            z, feas = qp.solve(A, np.concatenate([s.bl, bl]), np.concatenate([s.bu, bu]),
+                               np.concatenate([s.lb, np.zeros(N)]), np.concatenate([s.ub, np.full(N, np.inf)]),
+                               q, np.zeros(n + N))
+            if not feas:
+                raise RuntimeError("oracle: infeasible scenario %s" % s.name)
+            self.x[k] = z[:n]
+            self.xsq[k] = z[n:]
+            self.obj[k] = self.scen_objective(k, self.x[k])
+
+    def scen_objective(self, k, x):
+        s = self.scens[k]
+        f = float(np.dot(s.c, x)) + s.c0
+        xn = x[self.ncol[k]]
+        if self.W_on:
+            f += float(np.dot(self.W[k], xn))
+        if self.prox_on:
+            xb = self.xbar[k]
+            f += float(np.sum(self.rho[k] / 2.0 * (self.xsq[k] - 2.0 * xb * xn + xb ** 2)))
+        return f
