@@ -64,7 +64,7 @@ struct WgPairs {
     // inverse factor depend on A (fixed), the active set (column and row codes)
     // and the prox weights pN + the regularisation; they change little from one
     // PH iteration to the next, so the factor of the last set a scenario solved
-    // with is kept (its explicit L^-1 and 1/diag) under that key and reused
+    // with is kept (its explicit L^-1, lower triangle) under that key and reused
     // when a round's active set and weights match it bit for bit.
     double* fac;          // [S][fac_stride]: L^-1 (ma x ld, rows) then dg (ma)
     int64_t fac_stride;
@@ -299,9 +299,12 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
             if (diff) L.flag[1] = 1;
             WG_SYNC();
             if (L.flag[1] == 0) {
+                // (the refinement reads only L^-1, the lower triangle)
                 const double* f = G.fac + (int64_t)s * G.fac_stride;
-                for (int e = WG_TID; e < ma * ld; e += WG_NT) L.Sm[e] = f[e];
-                for (int e = WG_TID; e < ma; e += WG_NT) L.dg[e] = f[(int64_t)ma * ld + e];
+                for (int e = WG_TID; e < ma * ld; e += WG_NT) {
+                    const int i = e / ld, c = e - i * ld;
+                    if (c <= i) L.Sm[e] = f[e];
+                }
                 WG_SYNC();
                 WG_CNT(10);
                 reused = true;
@@ -380,21 +383,6 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
             }
             WG_SYNC();
             WG_TP(3);
-            if (cache) {
-                // keep this set's factor for the next solve of the scenario
-                double* f = G.fac + (int64_t)s * G.fac_stride;
-                for (int e = WG_TID; e < ma * ld; e += WG_NT) f[e] = L.Sm[e];
-                for (int e = WG_TID; e < ma; e += WG_NT) f[(int64_t)ma * ld + e] = L.dg[e];
-                int8_t* kc = G.key + (int64_t)s * G.key_stride;
-                double* pk = G.pkey + (int64_t)s * (G.N + 1);
-                for (int j = WG_TID; j < n; j += WG_NT) kc[j] = L.cc[j];
-                for (int i = WG_TID; i < m; i += WG_NT) kc[n + i] = L.rc[i];
-                for (int t = WG_TID; t < G.N; t += WG_NT) pk[t] = P.pN[ix(t, s, S)];
-                if (WG_TID == 0) {
-                    pk[G.N] = reg;
-                    G.ok[s] = 1;
-                }
-            }
         }
         // ---- iterative refinement on the unregularised KKT (a proximal-point
         //      iteration) ----
@@ -511,7 +499,29 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
         if (bad) L.flag[0] = 1;
         WG_SYNC();
         WG_TP(5);
-        if (L.flag[0] == 0) return round + 1;
+        if (L.flag[0] == 0) {
+            if (cache && !reused) {
+                // keep the certified set's factor (L^-1, lower triangle) for the
+                // scenario's next solve -- only the final round's: the earlier
+                // rounds' sets are left behind (storing every round's wrote 4x
+                // the bytes of the whole solve's inputs and outputs, PMC r03 s16)
+                double* f = G.fac + (int64_t)s * G.fac_stride;
+                for (int e = WG_TID; e < ma * ld; e += WG_NT) {
+                    const int i = e / ld, c = e - i * ld;
+                    if (c <= i) f[e] = L.Sm[e];
+                }
+                int8_t* kc = G.key + (int64_t)s * G.key_stride;
+                double* pk = G.pkey + (int64_t)s * (G.N + 1);
+                for (int j = WG_TID; j < n; j += WG_NT) kc[j] = L.cc[j];
+                for (int i = WG_TID; i < m; i += WG_NT) kc[n + i] = L.rc[i];
+                for (int t = WG_TID; t < G.N; t += WG_NT) pk[t] = P.pN[ix(t, s, S)];
+                if (WG_TID == 0) {
+                    pk[G.N] = reg;
+                    G.ok[s] = 1;
+                }
+            }
+            return round + 1;
+        }
         if (round + 1 == rounds) break;
         // ---- primal-dual active-set update: wrong-signed multipliers leave,
         //      violated bounds and rows enter ----

@@ -45,5 +45,10 @@ case "$1" in
           "pmc:r03_s16_c2_fetch:FETCH_SIZE:--only C2 $A" "pmc:r03_s16_c2_write:WRITE_SIZE:--only C2 $A" \
           "pmc:r03_s16_c5a_fetch:FETCH_SIZE:--only C5a $A" "pmc:r03_s16_c5a_write:WRITE_SIZE:--only C5a $A" \
           "pmc:r03_s16_c5b_fetch:FETCH_SIZE:--only C5b $A" "pmc:r03_s16_c5b_write:WRITE_SIZE:--only C5b $A" ;;
+  s17) $J "test:tests/test_prox_approx.py tests/test_cylinders.py tests/test_abi_layout.py tests/test_gpu_parity.py" \
+          "bench:r03_s17_c2:--only C2 $A" "bench:r03_s17_c5a:--only C5a $A" \
+          "pmc:r03_s17_c2_fetch:FETCH_SIZE:--only C2 $A" "pmc:r03_s17_c2_write:WRITE_SIZE:--only C2 $A" \
+          "pmc:r03_s17_c5a_write:WRITE_SIZE:--only C5a $A" ;;
+  s18) $J "test:tests" "bench:r03_s18_bench_default:" "prof:r03_s18_prof:$H --ar-probe 0" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac

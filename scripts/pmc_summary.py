@@ -2,10 +2,11 @@
 with the gfx950 FETCH_SIZE correction (MI355X_MICROARCH.md, HBM section:
 FETCH_SIZE reports half the bytes of a coalesced streaming read -> x2).
 
-    python scripts/pmc_summary.py KERNEL [--last N] dir1 [dir2 ...] > profiles/xxx.json
+    python scripts/pmc_summary.py KERNEL [--last N] [--skip-idle] dir1 [dir2 ...] > profiles/xxx.json
 
 --last N keeps the last N launches of KERNEL in each pass (by dispatch id): the
 timed window of a bench run that ends with its timed iterations (--no-conv).
+--skip-idle drops launches below 1 % of the largest (phx_iterk's gated launches).
 """
 import collections
 import csv
@@ -40,6 +41,11 @@ def add(agg, out, last):
     """per-dispatch sums -> mean over the (last) launches"""
     for k, per in agg.items():
         v = [per[i] for i in sorted(per)]
+        if SKIP_IDLE and v:
+            # gated launches (phx_iterk's pipeline past its stop: the kernel
+            # exits at its first load) are not solves
+            top = max(v)
+            v = [x for x in v if x >= 0.01 * top]
         if last:
             v = v[-last:]
         out["counters"][k] = sum(v) / len(v)
@@ -55,9 +61,14 @@ def finish(out):
     print(json.dumps(out, indent=1))
 
 
+SKIP_IDLE = False
+
 if __name__ == "__main__":
     a = sys.argv[1:]
     last = None
+    if "--skip-idle" in a:
+        a.remove("--skip-idle")
+        SKIP_IDLE = True
     if "--last" in a:
         i = a.index("--last")
         last = int(a[i + 1])
