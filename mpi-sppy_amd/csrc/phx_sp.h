@@ -95,26 +95,36 @@ struct SpLds {
     double *red;   // [8 * SP_RED] reduction slots
 };
 
-PHX_HD size_t sp_lds_bytes(int n, int m, int nC, int nlink) {
+// Split layout (split = true): the link / B-row / column vectors (lv, Mbb,
+// hv, xv: nlink + m + 2n doubles) live in the workgroup's global scratch slot
+// instead of LDS, so that more workgroups fit a CU (netdes 50-30-H: 129 KB of
+// LDS per workgroup, one per CU, against 46 KB, three).
+PHX_HD size_t sp_split_doubles(int n, int m, int nlink) {
+    return (size_t)nlink + (size_t)m + 2 * (size_t)n;
+}
+
+PHX_HD size_t sp_lds_bytes(int n, int m, int nC, int nlink, bool split = false) {
     const size_t ld = (size_t)(nC | 1);
-    const size_t d = (size_t)nC * ld + 2 * (size_t)nC + (size_t)nlink + (size_t)m + 2 * (size_t)n +
-                     2 * (size_t)m + 8 * SP_RED;
+    size_t d = (size_t)nC * ld + 2 * (size_t)nC + 2 * (size_t)m + 8 * SP_RED;
+    if (!split) d += sp_split_doubles(n, m, nlink);
     return d * 8;
 }
 
-PHX_HD SpLds sp_carve(double* base, int n, int m, int nC, int nlink) {
+// gbase: the split vectors' place (null: LDS, after the rest)
+PHX_HD SpLds sp_carve(double* base, int n, int m, int nC, int nlink, double* gbase = nullptr) {
     SpLds L;
     double* d = base;
     L.red = d; d += 8 * SP_RED;
     L.Sm = d; d += (size_t)nC * (nC | 1);
     L.dg = d; d += nC;
     L.cv = d; d += nC;
-    L.lv = d; d += nlink;
-    L.Mbb = d; d += m;
-    L.hv = d; d += n;
-    L.xv = d; d += n;
     L.yv = d; d += m;
     L.tv = d; d += m;
+    double* g = gbase ? gbase : d;
+    L.lv = g; g += nlink;
+    L.Mbb = g; g += m;
+    L.hv = g; g += n;
+    L.xv = g; g += n;
     return L;
 }
 

@@ -50,5 +50,7 @@ case "$1" in
           "pmc:r03_s17_c2_fetch:FETCH_SIZE:--only C2 $A" "pmc:r03_s17_c2_write:WRITE_SIZE:--only C2 $A" \
           "pmc:r03_s17_c5a_write:WRITE_SIZE:--only C5a $A" ;;
   s18) $J "test:tests" "bench:r03_s18_bench_default:" "prof:r03_s18_prof:$H --ar-probe 0" ;;
+  s19) $J "test:tests/test_netdes.py tests/test_sslp.py tests/test_trajectories.py" \
+          "bench:r03_s19_c5b_split:--only C5b $A" && PHX_SP_SPLIT=0 $J "bench:r03_s19_c5b_nosplit:--only C5b $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
