@@ -52,5 +52,8 @@ case "$1" in
   s18) $J "test:tests" "bench:r03_s18_bench_default:" "prof:r03_s18_prof:$H --ar-probe 0" ;;
   s19) $J "test:tests/test_netdes.py tests/test_sslp.py tests/test_trajectories.py" \
           "bench:r03_s19_c5b_split:--only C5b $A" && PHX_SP_SPLIT=0 $J "bench:r03_s19_c5b_nosplit:--only C5b $A" ;;
+  s20) $J "pmc:r03_s20_c5a_fetch:FETCH_SIZE:--only C5a $A" "pmc:r03_s20_c5a_write:WRITE_SIZE:--only C5a $A" \
+          "pmc:r03_s20_c5b_fetch:FETCH_SIZE:--only C5b $A" "pmc:r03_s20_c5b_write:WRITE_SIZE:--only C5b $A" \
+          "pmc:r03_s20_c4_fetch:FETCH_SIZE:--only C4 $A" "pmc:r03_s20_c4_write:WRITE_SIZE:--only C4 $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
