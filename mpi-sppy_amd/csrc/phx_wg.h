@@ -73,6 +73,8 @@ struct WgPairs {
     double* pkey;         // [S][N+1]: pN of the nonant slots, then reg
     int32_t* ok;          // [S]: the cached factor is valid
     int32_t N;
+    char* split;          // [S][split_stride] wg_carve's split arrays, or null (all in LDS)
+    int64_t split_stride;
 };
 
 // Carve of the dynamic LDS of one scenario.
@@ -87,14 +89,25 @@ struct WgLds {
     int8_t *cc, *rc;   // column code 0 free / 1 at l / 2 at u; row code 0 inactive / 1 at bl / 2 at bu
 };
 
-PHX_HD size_t wg_lds_bytes(int n, int m, int nnz) {
+// Split layout (split = true): the scenario's A values, the column vectors
+// (xp, r1, qq, pp) and the CSC row / position indices (ri, c2) live in a
+// per-scenario global scratch area (wg_split_bytes) instead of LDS, so that
+// more workgroups fit a CU (sslp_15_45: 75 KB of LDS, two per CU, against
+// 37 KB, four).
+PHX_HD size_t wg_split_bytes(int n, int nnz) {
+    return (8 * ((size_t)nnz + 4 * (size_t)n) + 4 * (size_t)nnz + 15) & ~(size_t)15;
+}
+
+PHX_HD size_t wg_lds_bytes(int n, int m, int nnz, bool split = false) {
     if (n >= 32767 || m >= 32767 || nnz >= 32767) return ~(size_t)0;   // 16-bit indices
-    size_t b = 8 * ((size_t)m * (m + 1) + 4 * (size_t)m + (size_t)nnz + 4 * (size_t)n) + 16 + 64 +
-               2 * ((size_t)n + 1 + 3 * (size_t)nnz + (size_t)m + 1 + 2 * (size_t)m) + (size_t)n + (size_t)m;
+    const size_t moved_d = split ? 0 : (size_t)nnz + 4 * (size_t)n;
+    const size_t idx16 = (size_t)n + 1 + (split ? 1 : 3) * (size_t)nnz + (size_t)m + 1 + 2 * (size_t)m;
+    size_t b = 8 * ((size_t)m * (m + 1) + 4 * (size_t)m + moved_d) + 16 + 64 + 2 * idx16 + (size_t)n + (size_t)m;
     return (b + 15) & ~(size_t)15;
 }
 
-PHX_HD WgLds wg_carve(void* base, int n, int m, int nnz) {
+// gbase: the split arrays' place (null: everything in LDS)
+PHX_HD WgLds wg_carve(void* base, int n, int m, int nnz, void* gbase = nullptr) {
     WgLds L;
     double* d = (double*)base;
     L.Sm = d; d += (size_t)m * (m + 1);   // rows padded to an odd stride (wg_warm)
@@ -102,17 +115,20 @@ PHX_HD WgLds wg_carve(void* base, int n, int m, int nnz) {
     L.z = d; d += m;
     L.t = d; d += m;
     L.u = d; d += m;
-    L.a = d; d += nnz;
-    L.xp = d; d += n;
-    L.r1 = d; d += n;
-    L.qq = d; d += n;
-    L.pp = d; d += n;
+    double* g = gbase ? (double*)gbase : d;
+    L.a = g; g += nnz;
+    L.xp = g; g += n;
+    L.r1 = g; g += n;
+    L.qq = g; g += n;
+    L.pp = g; g += n;
+    if (!gbase) d = g;
     L.red = d; d += 8;
     L.flag = (int32_t*)d;
     int16_t* w = (int16_t*)(L.flag + 4);
+    int16_t* gw = gbase ? (int16_t*)g : nullptr;
     L.cp = w; w += n + 1;
-    L.ri = w; w += nnz;
-    L.c2 = w; w += nnz;
+    if (gw) { L.ri = gw; gw += nnz; L.c2 = gw; gw += nnz; }
+    else { L.ri = w; w += nnz; L.c2 = w; w += nnz; }
     L.rp = w; w += m + 1;
     L.ci = w; w += nnz;
     L.ar = w; w += m;

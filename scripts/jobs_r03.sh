@@ -55,5 +55,8 @@ case "$1" in
   s20) $J "pmc:r03_s20_c5a_fetch:FETCH_SIZE:--only C5a $A" "pmc:r03_s20_c5a_write:WRITE_SIZE:--only C5a $A" \
           "pmc:r03_s20_c5b_fetch:FETCH_SIZE:--only C5b $A" "pmc:r03_s20_c5b_write:WRITE_SIZE:--only C5b $A" \
           "pmc:r03_s20_c4_fetch:FETCH_SIZE:--only C4 $A" "pmc:r03_s20_c4_write:WRITE_SIZE:--only C4 $A" ;;
+  s21) $J "test:tests/test_sslp.py tests/test_gpu_parity.py tests/test_trajectories.py" \
+          "bench:r03_s21_c5a_split:--only C5a $A" "bench:r03_s21_c2:--only C2 $A" && \
+       PHX_WG_SPLIT=0 $J "bench:r03_s21_c5a_nosplit:--only C5a $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
