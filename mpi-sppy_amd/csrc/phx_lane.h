@@ -199,6 +199,16 @@ __device__ __forceinline__ void lane_stamp(const LaneIO& io, int k) {
 }
 #endif
 
+// Per-lane output stores.  PHX_OUT_WT: write-through (`sc1`, agent-scope
+// relaxed atomic stores), which leave no dirty L2 line behind -- a dependent
+// kernel boundary costs ~1.7 us + the dirty bytes / 6 TB/s (MI355X_MICROARCH.md,
+// "boundary"), and a warm pass leaves ~23 MB of outputs dirty.
+#if (defined(__HIPCC__) || defined(__HIPCC_RTC__)) && defined(PHX_OUT_WT)
+#define PHX_OUT(lv, v) __hip_atomic_store(&(lv), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+#else
+#define PHX_OUT(lv, v) ((lv) = (v))
+#endif
+
 // phx_iterk gate: every kernel of an iteration past the device-side stop exits
 // at once (one scalar load; the counters stay as the last real solve left them)
 PHX_LD bool gated(const int32_t* gate) { return gate && *(const volatile int32_t*)gate; }
@@ -765,7 +775,7 @@ PHX_LD void aset_store(const LaneIO& io, int sc, const ASet<PT>& a) {
     // (the word addresses recomputed from an opaque index: kept from aset_load
     // across the solve they were spilled to scratch)
     const int so = opaque_index(sc);
-    PHX_UNROLL for (int k = 0; k < aset_words(PT::n(), PT::m()); ++k) io.aset[(int64_t)k * io.S + so] = w[k];
+    PHX_UNROLL for (int k = 0; k < aset_words(PT::n(), PT::m()); ++k) PHX_OUT(io.aset[(int64_t)k * io.S + so], w[k]);
 }
 
 // Classify at an interior-point (x, y): a bound/row is active when its slack
@@ -1260,18 +1270,18 @@ PHX_LD void write_certified(const LaneIO& io, const Data<PT>& D, int sc, const A
     double f = D.kn;
     PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
         const double xu = xp[j] * D.dc(j);
-        io.x_out[(int64_t)j * S + sc] = xu;
+        PHX_OUT(io.x_out[(int64_t)j * S + sc], xu);
         f += D.c(j) * xp[j];
         if (PT::col_slot(j) >= 0) f += D.qn[PT::col_slot(j)] * xu + 0.5 * D.pn[PT::col_slot(j)] * xu * xu;
     }
     if (io.y_out)
-        PHX_UNROLL for (int i = 0; i < PT::m(); ++i) io.y_out[(int64_t)i * S + sc] = -z[i] * D.dr(i);
-    io.obj_out[sc] = f;
-    io.status[sc] = 1;
-    io.iters[sc] = its;
-    if (io.status_out) io.status_out[sc] = 1;
-    if (io.iters_out) io.iters_out[sc] = its;
-    io.flags[sc] = (its > 0 ? (FLAG_WRITTEN | FLAG_IPM_TRIED) : FLAG_WRITTEN) | (map_ok ? FLAG_MAP : 0);
+        PHX_UNROLL for (int i = 0; i < PT::m(); ++i) PHX_OUT(io.y_out[(int64_t)i * S + sc], -z[i] * D.dr(i));
+    PHX_OUT(io.obj_out[sc], f);
+    PHX_OUT(io.status[sc], 1);
+    PHX_OUT(io.iters[sc], its);
+    if (io.status_out) PHX_OUT(io.status_out[sc], 1);
+    if (io.iters_out) PHX_OUT(io.iters_out[sc], its);
+    PHX_OUT(io.flags[sc], (its > 0 ? (FLAG_WRITTEN | FLAG_IPM_TRIED) : FLAG_WRITTEN) | (map_ok ? FLAG_MAP : 0));
     aset_store<PT>(io, sc, a);
 }
 
@@ -1524,7 +1534,7 @@ __device__ double fz_update_w(const LaneIO& io, int sc) {
         if (t >= 0) {
             const int64_t o = (int64_t)t * S + sc;
             const double diff = f.x_prev[(int64_t)j * S + sc] - f.stage[io.xbar_idx[o]];
-            const_cast<double*>(io.W)[o] = io.W[o] + io.rho[o] * diff;
+            PHX_OUT(const_cast<double*>(io.W)[o], io.W[o] + io.rho[o] * diff);
             d += fabs(diff);
         }
     }

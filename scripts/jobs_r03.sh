@@ -58,5 +58,9 @@ case "$1" in
   s21) $J "test:tests/test_sslp.py tests/test_gpu_parity.py tests/test_trajectories.py" \
           "bench:r03_s21_c5a_split:--only C5a $A" "bench:r03_s21_c2:--only C2 $A" && \
        PHX_WG_SPLIT=0 $J "bench:r03_s21_c5a_nosplit:--only C5a $A" ;;
+  s22) $J "bench:r03_s22_base1:$H --ar-probe 0" "bench:r03_s22_base50:$B --ar-probe 0" && \
+       PHX_LANE_DEFS=PHX_OUT_WT $J "bench:r03_s22_wt1:$H --ar-probe 0" "bench:r03_s22_wt50:$B --ar-probe 0" \
+          "prof:r03_s22_wt_prof:$H --ar-probe 0" && \
+       $J "bench:r03_s22_base2:$H --ar-probe 0" && PHX_LANE_DEFS=PHX_OUT_WT $J "bench:r03_s22_wt2:$H --ar-probe 0" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
