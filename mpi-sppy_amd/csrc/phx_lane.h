@@ -199,11 +199,13 @@ __device__ __forceinline__ void lane_stamp(const LaneIO& io, int k) {
 }
 #endif
 
-// Per-lane output stores.  PHX_OUT_WT: write-through (`sc1`, agent-scope
-// relaxed atomic stores), which leave no dirty L2 line behind -- a dependent
-// kernel boundary costs ~1.7 us + the dirty bytes / 6 TB/s (MI355X_MICROARCH.md,
-// "boundary"), and a warm pass leaves ~23 MB of outputs dirty.
-#if (defined(__HIPCC__) || defined(__HIPCC_RTC__)) && defined(PHX_OUT_WT)
+// Per-lane output stores: write-through (`sc1`, agent-scope relaxed atomic
+// stores), which leave no dirty L2 line behind -- a dependent kernel boundary
+// costs ~1.7 us + the dirty bytes / 6 TB/s (MI355X_MICROARCH.md, "boundary"),
+// and a warm pass writes ~23 MB.  Measured (r03 s22, farmer 100k): warm kernel
+// 40.8 -> 39.2 us by events, 1.11 -> 1.13 x 10^9 at K = 20, 1.62 -> 1.65 x 10^9
+// at K = 50.  PHX_OUT_PLAIN (a JIT define, PHX_LANE_DEFS) restores plain stores.
+#if (defined(__HIPCC__) || defined(__HIPCC_RTC__)) && !defined(PHX_OUT_PLAIN)
 #define PHX_OUT(lv, v) __hip_atomic_store(&(lv), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
 #else
 #define PHX_OUT(lv, v) ((lv) = (v))
