@@ -62,5 +62,7 @@ case "$1" in
        PHX_LANE_DEFS=PHX_OUT_WT $J "bench:r03_s22_wt1:$H --ar-probe 0" "bench:r03_s22_wt50:$B --ar-probe 0" \
           "prof:r03_s22_wt_prof:$H --ar-probe 0" && \
        $J "bench:r03_s22_base2:$H --ar-probe 0" && PHX_LANE_DEFS=PHX_OUT_WT $J "bench:r03_s22_wt2:$H --ar-probe 0" ;;
+  s23) $J "test:tests" "bench:r03_s23_bench_default:" "prof:r03_s23_prof:$H --ar-probe 0" \
+          "pmc:r03_s23_pmc_fetch:FETCH_SIZE:$B" "pmc:r03_s23_pmc_write:WRITE_SIZE:$B" "pmc:r03_s23_pmc_sq:$SQ:$B" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
