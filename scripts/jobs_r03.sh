@@ -64,7 +64,7 @@ case "$1" in
        $J "bench:r03_s22_base2:$H --ar-probe 0" && PHX_LANE_DEFS=PHX_OUT_WT $J "bench:r03_s22_wt2:$H --ar-probe 0" ;;
   s23) $J "test:tests" "bench:r03_s23_bench_default:" "prof:r03_s23_prof:$H --ar-probe 0" \
           "pmc:r03_s23_pmc_fetch:FETCH_SIZE:$B" "pmc:r03_s23_pmc_write:WRITE_SIZE:$B" "pmc:r03_s23_pmc_sq:$SQ:$B" ;;
-  s24) $J "test:tests/test_netdes.py tests/test_sslp.py tests/test_trajectories.py tests/test_gpu_parity.py -k 'sp or netdes or sslp or cm10 or wg or trajectory'" \
+  s24) $J "test:tests/test_netdes.py tests/test_sslp.py tests/test_trajectories.py tests/test_gpu_parity.py" \
           "bench:r03_s24_c2:--only C2 $A" "bench:r03_s24_c5b:--only C5b $A" "bench:r03_s24_c5a:--only C5a $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
