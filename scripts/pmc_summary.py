@@ -17,13 +17,22 @@ import sqlite3
 import sys
 
 
+def base_name(name):
+    """'void k_wg_warm<false>(phx::Prob, ...)' -> 'k_wg_warm' (template kernels
+    count under their template's name)."""
+    n = name.split("(")[0].strip()
+    if n.startswith("void "):
+        n = n[5:]
+    return n.split("<")[0]
+
+
 def main(kernel, dirs, last=None):
     out = {"kernel": kernel, "counters": {}, "launches": {}, "window": "last %d launches" % last if last else "all"}
     for d in dirs:
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             agg = collections.defaultdict(lambda: collections.defaultdict(float))
             for r in csv.DictReader(open(f)):
-                if r["Kernel_Name"].split("(")[0] == kernel:
+                if base_name(r["Kernel_Name"]) == kernel:
                     agg[r["Counter_Name"]][int(r["Dispatch_Id"])] += float(r["Counter_Value"])
             add(agg, out, last)
         for f in glob.glob(os.path.join(d, "**", "*results.db"), recursive=True):
@@ -31,7 +40,7 @@ def main(kernel, dirs, last=None):
             con = sqlite3.connect(f)
             for name, disp, ctr, val in con.execute(
                     "select kernel_name, dispatch_id, counter_name, value from counters_collection"):
-                if name.split("(")[0] == kernel:
+                if base_name(name) == kernel:
                     agg[ctr][int(disp)] += float(val)
             add(agg, out, last)
     finish(out)
