@@ -66,5 +66,6 @@ case "$1" in
           "pmc:r03_s23_pmc_fetch:FETCH_SIZE:$B" "pmc:r03_s23_pmc_write:WRITE_SIZE:$B" "pmc:r03_s23_pmc_sq:$SQ:$B" ;;
   s24) $J "test:tests/test_netdes.py tests/test_sslp.py tests/test_trajectories.py tests/test_gpu_parity.py" \
           "bench:r03_s24_c2:--only C2 $A" "bench:r03_s24_c5b:--only C5b $A" "bench:r03_s24_c5a:--only C5a $A" ;;
+  s25) $J "prof:r03_s25_c2_prof:--only C2 $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
