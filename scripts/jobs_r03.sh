@@ -67,5 +67,7 @@ case "$1" in
   s24) $J "test:tests/test_netdes.py tests/test_sslp.py tests/test_trajectories.py tests/test_gpu_parity.py" \
           "bench:r03_s24_c2:--only C2 $A" "bench:r03_s24_c5b:--only C5b $A" "bench:r03_s24_c5a:--only C5a $A" ;;
   s25) $J "prof:r03_s25_c2_prof:--only C2 $A" ;;
+  s26) $J "test:tests/test_gpu_parity.py tests/test_trajectories.py tests/test_hydro.py" \
+          "bench:r03_s26_c2:--only C2 $A" "bench:r03_s26_c4:--only C4 $A" "prof:r03_s26_c2_prof:--only C2 $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
