@@ -354,7 +354,46 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
             // one pivot's update is spread over 4x as many threads; the pivot
             // row element lij is read by all four, written by none of them)
             bool spd = true;
-            for (int jj = 0; jj < ma; ++jj) {
+            // pivots in pairs (a, b = a+1), one barrier per pair: the second
+            // pivot's column and diagonal are corrected for the first on the
+            // fly with the very expressions the one-pivot step would store
+            // (row k col b: Sm[k][b] - (Sm[k][a] / d_a) * Sm[b][a]), so the
+            // factor is the same; half the barriers and row round trips
+            int j2 = 0;
+            for (; j2 + 1 < ma; j2 += 2) {
+                const int a = j2, b = j2 + 1;
+                const double d0 = L.Sm[a * ld + a];
+                if (!(d0 > 0.0)) { spd = false; break; }
+                const double e = L.Sm[b * ld + a], id0 = 1.0 / d0;
+                const double d1 = L.Sm[b * ld + b] - (e * id0) * e;
+                if (!(d1 > 0.0)) { spd = false; break; }
+                const double sd0 = sqrt(d0), sd1 = sqrt(d1), id1 = 1.0 / d1;
+                for (int i = b + 1 + WG_QID; i < ma; i += WG_QN) {
+                    double* row = L.Sm + (size_t)i * ld;
+                    const double lia = row[a];
+                    const double f0 = lia * id0;
+                    const double lib = row[b] - f0 * e;
+                    const double f1 = lib * id1;
+                    int k = b + 1 + WG_QL;
+                    for (; k <= i; k += WG_QW) {
+                        const double ga = L.Sm[k * ld + a];
+                        const double h = L.Sm[k * ld + b] - (ga * id0) * e;
+                        const double t = row[k] - f0 * ga;
+                        row[k] = t - f1 * h;
+                    }
+                    if (WG_QL == 0) {
+                        L.Sm[a * ld + i] = lia / sd0;
+                        L.Sm[b * ld + i] = lib / sd1;
+                    }
+                }
+                if (WG_TID == 0) {
+                    L.dg[a] = 1.0 / sd0;
+                    L.dg[b] = 1.0 / sd1;
+                    L.Sm[a * ld + b] = e / sd0;
+                }
+                WG_SYNC();
+            }
+            for (int jj = spd ? j2 : ma; jj < ma; ++jj) {
                 const double d = L.Sm[jj * ld + jj];
                 if (!(d > 0.0)) { spd = false; break; }
                 const double sd = sqrt(d), id = 1.0 / d;

@@ -70,7 +70,7 @@ case "$1" in
   s26) $J "test:tests/test_gpu_parity.py tests/test_trajectories.py tests/test_hydro.py" \
           "bench:r03_s26_c2:--only C2 $A" "bench:r03_s26_c4:--only C4 $A" "prof:r03_s26_c2_prof:--only C2 $A" ;;
   s27) $J "test:tests" "bench:r03_s27_bench_default:" "prof:r03_s27_c2_prof:--only C2 $A" ;;
-  s28) $J "test:tests/test_gpu_parity.py tests/test_trajectories.py tests/test_prox_approx.py" \
-          "bench:r03_s28_c2:--only C2 $A" "bench:r03_s28_c4:--only C4 $A" "prof:r03_s28_c2_prof:--only C2 $A" ;;
+  s28) $J "test:tests/test_gpu_parity.py tests/test_trajectories.py tests/test_prox_approx.py tests/test_sslp.py" \
+          "bench:r03_s28_c2:--only C2 $A" "bench:r03_s28_c4:--only C4 $A" "bench:r03_s28_c5a:--only C5a $A" "prof:r03_s28_c2_prof:--only C2 $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
