@@ -243,8 +243,52 @@ PHX_HD bool sp_factor(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds
     }
     SP_SYNC();
     // right-looking Cholesky, every trailing entry its own work item; L[i][k]
-    // (i > k) is stored transposed at Sm[k*ld + i], 1/L_kk in dg
-    for (int jj = 0; jj < nC; ++jj) {
+    // (i > k) is stored transposed at Sm[k*ld + i], 1/L_kk in dg.
+    // Pivots in pairs (a, b = a+1), one barrier per pair: every trailing
+    // entry applies both updates, with b's column and diagonal corrected for a
+    // by the very expressions the one-pivot step stores (the same factor)
+    int j2 = 0;
+    for (; j2 + 1 < nC; j2 += 2) {
+        const int a = j2, b = j2 + 1;
+        double d0 = L.Sm[a * ld + a];
+        if (ipm_safe) {
+            const double c0 = L.cv[a];
+            if (!(c0 > 0.0 && c0 < 1e300)) return false;
+            if (!(d0 > 1e-13 * c0)) d0 = 1e128;
+        }
+        if (!(d0 > 0.0)) return false;
+        const double e = L.Sm[b * ld + a], id0 = 1.0 / d0;
+        double d1 = L.Sm[b * ld + b] - e * e * id0;
+        if (ipm_safe) {
+            const double c1 = L.cv[b];
+            if (!(c1 > 0.0 && c1 < 1e300)) return false;
+            if (!(d1 > 1e-13 * c1)) d1 = 1e128;
+        }
+        if (!(d1 > 0.0)) return false;
+        const double sd0 = sqrt(d0), sd1 = sqrt(d1), id1 = 1.0 / d1;
+        const int R = nC - b - 1;
+        for (int p = SP_TID; p < R * R; p += SP_NT) {
+            const int i = b + 1 + p / R, k = b + 1 + (p - (p / R) * R);
+            if (k > i) continue;
+            const double sia = L.Sm[i * ld + a];
+            const double sib = L.Sm[i * ld + b] - sia * e * id0;
+            if (k == i) {
+                L.Sm[a * ld + i] = sia / sd0;
+                L.Sm[b * ld + i] = sib / sd1;
+            }
+            const double ska = L.Sm[k * ld + a];
+            const double hk = L.Sm[k * ld + b] - ska * e * id0;
+            const double t = L.Sm[i * ld + k] - sia * ska * id0;
+            L.Sm[i * ld + k] = t - sib * hk * id1;
+        }
+        if (SP_TID == 0) {
+            L.dg[a] = 1.0 / sd0;
+            L.dg[b] = 1.0 / sd1;
+            L.Sm[a * ld + b] = e / sd0;
+        }
+        SP_SYNC();
+    }
+    for (int jj = j2; jj < nC; ++jj) {
         double d = L.Sm[jj * ld + jj];
         if (ipm_safe) {
             const double d0 = L.cv[jj];

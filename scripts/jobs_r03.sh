@@ -72,5 +72,7 @@ case "$1" in
   s27) $J "test:tests" "bench:r03_s27_bench_default:" "prof:r03_s27_c2_prof:--only C2 $A" ;;
   s28) $J "test:tests/test_gpu_parity.py tests/test_trajectories.py tests/test_prox_approx.py tests/test_sslp.py" \
           "bench:r03_s28_c2:--only C2 $A" "bench:r03_s28_c4:--only C4 $A" "bench:r03_s28_c5a:--only C5a $A" "prof:r03_s28_c2_prof:--only C2 $A" ;;
+  s29) $J "test:tests/test_netdes.py tests/test_sslp.py tests/test_gpu_parity.py tests/test_trajectories.py" \
+          "bench:r03_s29_c5b:--only C5b $A" "bench:r03_s29_c2:--only C2 $A" "bench:r03_s29_c5a:--only C5a $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
