@@ -74,5 +74,6 @@ case "$1" in
           "bench:r03_s28_c2:--only C2 $A" "bench:r03_s28_c4:--only C4 $A" "bench:r03_s28_c5a:--only C5a $A" "prof:r03_s28_c2_prof:--only C2 $A" ;;
   s29) $J "test:tests/test_netdes.py tests/test_sslp.py tests/test_gpu_parity.py tests/test_trajectories.py" \
           "bench:r03_s29_c5b:--only C5b $A" "bench:r03_s29_c2:--only C2 $A" "bench:r03_s29_c5a:--only C5a $A" ;;
+  s30) $J "test:tests" "bench:r03_s30_bench_default:" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
