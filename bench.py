@@ -33,11 +33,14 @@ Inputs resident in HBM before timing.  Extra keys:
                 one worker process per core) on a bounded sample, child process,
                 rank 0 at N = 1
   configs       (N = 1) the other BASELINE configs, each timed the same way
-                (Iter0 + K' iterations): C3x1M farmer x 1,000,000 (the over-cache
-                HBM configuration), C2 farmer crops_multiplier=10 x 1,000,
-                C4 aircond 10x10x10, C5a sslp_15_45 x 10,000, C5b netdes
-                network-50-30-H x 10,000 — value, steady state, dominant kernel
-                + roofline, CPU baseline
+                (Iter0 + K' iterations): C1 farmer x 3 (configs[0]), C3s8 farmer x
+                12,500 (the 8-GPU per-rank slice of configs[2]), C3x1M farmer x
+                1,000,000 (the over-cache HBM configuration), C2 farmer
+                crops_multiplier=10 x 1,000, C4 aircond 10x10x10, C5a sslp_15_45 x
+                10,000, C5b netdes network-50-30-H x 10,000 -- value, steady state,
+                dominant kernel + roofline (+ PMC traffic and its ratio to the
+                algorithmic bytes), CPU baseline (per-GPU share measured, whole host
+                projected)
 """
 import argparse
 import json
@@ -75,7 +78,7 @@ def parse():
     ap.add_argument("--cpu-scens", type=int, default=40000)
     ap.add_argument("--cpu-iters", type=int, default=6)
     ap.add_argument("--cpu-procs", type=int, default=16, help="worker processes (the GPU box's CPU share)")
-    ap.add_argument("--configs", default="all", help="'all', 'none' or a comma list of C3x1M,C2,C4,C5a,C5b")
+    ap.add_argument("--configs", default="all", help="'all', 'none' or a comma list of C1,C3s8,C3x1M,C2,C4,C5a,C5b")
     ap.add_argument("--config-steps", type=int, default=10, help="K' of the other configs")
     ap.add_argument("--only", default=None, help="run one config as the headline (C2, C4, C5a, C5b)")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
@@ -167,20 +170,37 @@ def sp_bytes(b):
 
 # profiles/r*_pmc_<tag>_<kernel>.json of each secondary config (scripts/pmc_summary.py
 # over the config's timed launches)
-CONFIG_PMC_TAG = {"C2": "farmercm10_1k", "C4": "aircond1k", "C5a": "sslp10k", "C5b": "netdes10k",
+CONFIG_PMC_TAG = {"C3s8": "farmer12k5", "C2": "farmercm10_1k", "C4": "aircond1k", "C5a": "sslp10k", "C5b": "netdes10k",
                   "C3x1M": "farmer1m"}
+
+
+def _current_source_hash(kernel):
+    sys.path.insert(0, os.path.join(_ROOT, "scripts"))
+    try:
+        import src_hash
+        return src_hash.source_hash(kernel)
+    finally:
+        sys.path.pop(0)
 
 
 def pmc_traffic(kernel, tag):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
     (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; scripts/pmc_summary.py): counters
-    need their own profiler runs, so they are read from profiles/ (newest first)."""
+    need their own profiler runs, so they are read from profiles/ (newest first).
+    Only a summary taken on the kernel's current sources counts (its
+    source_sha256, scripts/src_hash.py): an older one is reported as stale and
+    its bytes are not used.  Returns (bytes or None, file, status)."""
     import glob
     files = sorted(glob.glob(os.path.join(_ROOT, "profiles", "r*_pmc_%s_%s.json" % (tag, kernel))))
     if not files:
-        return None, None
+        return None, None, "no PMC summary"
     d = json.load(open(files[-1]))
-    return d.get("hbm_bytes_per_launch", {}).get("total"), os.path.relpath(files[-1], _ROOT)
+    src = os.path.relpath(files[-1], _ROOT)
+    cur = _current_source_hash(kernel)
+    if d.get("source_sha256") is None or d.get("source_sha256") != cur:
+        return None, src, "stale: measured on other %s sources (%s), current %s" % (
+            kernel, (d.get("source_sha256") or "unrecorded")[:12], (cur or "?")[:12])
+    return d.get("hbm_bytes_per_launch", {}).get("total"), src, "current (source_sha256 %s)" % cur[:12]
 
 
 def valu_issue(kernel, tag, units, avg_s, lanes_per_wave=64, simds=1024, clock_hz=2.4e9):
@@ -196,6 +216,9 @@ def valu_issue(kernel, tag, units, avg_s, lanes_per_wave=64, simds=1024, clock_h
     if not files or not avg_s:
         return None
     d = json.load(open(files[-1]))
+    if d.get("source_sha256") is None or d.get("source_sha256") != _current_source_hash(kernel):
+        return {"stale": True, "source": os.path.relpath(files[-1], _ROOT),
+                "note": "SQ counters measured on other %s sources: not used" % kernel}
     insts = d.get("counters", {}).get("SQ_INSTS_VALU")
     if not insts:
         return None
@@ -208,9 +231,18 @@ def valu_issue(kernel, tag, units, avg_s, lanes_per_wave=64, simds=1024, clock_h
             "source": os.path.relpath(files[-1], _ROOT)}
 
 
-def cpu_baseline(args, model="farmer", cm=1, scens=None, iters=None, total=None, timeout=900):
-    """oracle/cpu_bench.py in a child process (it never touches the GPU)."""
-    procs = max(1, min(args.cpu_procs, os.cpu_count() or 1))
+def cpu_baseline(args, model="farmer", cm=1, scens=None, iters=None, total=None, timeout=900, procs=None):
+    """oracle/cpu_bench.py in a child process (it never touches the GPU).
+
+    Measured with P worker processes = the GPU box's CPU share per GPU (16: the
+    pool's rule for worker pools on a one-GPU box), reported as
+    ``per_gpu_share``.  ``whole_host`` is BASELINE.md's bar -- the reference
+    under ``mpiexec -n P`` with P = all physical cores of the host -- projected
+    from that measurement by perfect linear scaling over the physical cores
+    (the subproblem solves are independent; the per-iteration reduction is a
+    few doubles), which can only overstate the host: running ~128 worker
+    processes on the box is outside its per-GPU CPU share."""
+    procs = max(1, min(procs or args.cpu_procs, os.cpu_count() or 1))
     cmd = [sys.executable, "-m", "oracle.cpu_bench", "--model", model, "--scens", str(scens or args.cpu_scens),
            "--iters", str(iters or args.cpu_iters), "--procs", str(procs), "--cm", str(cm), "--rho", str(args.rho)]
     if total:
@@ -222,7 +254,17 @@ def cpu_baseline(args, model="farmer", cm=1, scens=None, iters=None, total=None,
     if r.returncode != 0:
         return {"error": r.stderr[-500:]}
     d = json.loads(r.stdout.strip().splitlines()[-1])
-    return {k: d[k] for k in ["value", "unit", "cores", "kind", "sample", "seconds", "host"]}
+    out = {k: d[k] for k in ["value", "unit", "cores", "kind", "sample", "seconds", "host"]}
+    host = d.get("host") or {}
+    out["cpu_model"] = host.get("cpu_model")
+    out["per_gpu_share"] = {"value": d["value"], "cores": d["cores"], "measured": True}
+    phys = host.get("physical_cores")
+    if phys:
+        out["whole_host"] = {"value": d["value"] * phys / d["cores"], "cores": phys, "sockets": host.get("sockets"),
+                             "measured": False,
+                             "how": "per_gpu_share x physical cores / %d (perfect linear scaling: an upper bound "
+                                    "on the host)" % d["cores"]}
+    return out
 
 
 # ---------------------------------------------------------------- workloads
@@ -231,14 +273,24 @@ def workloads():
     from mpisppy_amd.utils import sputils
     bfs = [10, 10, 10]
     return {
+        "C1": dict(creator=farmer.scenario_creator, names=lambda S: farmer.scenario_names_creator(3),
+                   kw=lambda S, cm: {"num_scens": 3, "crops_multiplier": 1}, nodes=None, S=3,
+                   desc="farmer crops_multiplier=1, 3 scenarios, rho=1 (BASELINE configs[0]; the reference runs it "
+                        "under mpiexec -n 3)",
+                   cpu=dict(model="farmer", cm=1, scens=3, iters=10, total=3, procs=3)),
         "C3": dict(creator=farmer.scenario_creator, names=lambda S: farmer.scenario_names_creator(S),
                    kw=lambda S, cm: {"num_scens": S, "crops_multiplier": cm}, nodes=None,
                    desc="farmer crops_multiplier=%d, %d scenarios (BASELINE configs[2])"),
+        "C3s8": dict(creator=farmer.scenario_creator, names=lambda S: farmer.scenario_names_creator(12500),
+                     kw=lambda S, cm: {"num_scens": 12500, "crops_multiplier": 1}, nodes=None, S=12500, K=20,
+                     desc="farmer crops_multiplier=1, 12,500 scenarios on one GPU (the per-rank slice of "
+                          "configs[2] on 8 GPUs: 100,000 / 8)",
+                     cpu="headline"),
         "C3x1M": dict(creator=farmer.scenario_creator, names=lambda S: farmer.scenario_names_creator(1000000),
                       kw=lambda S, cm: {"num_scens": 1000000, "crops_multiplier": 1}, nodes=None, S=1000000,
                       desc="farmer crops_multiplier=1, 1,000,000 scenarios on one GPU (the over-cache HBM "
                            "configuration of configs[2]: working set > 256 MiB Infinity Cache)",
-                      cpu=None),
+                      cpu="headline"),
         "C2": dict(creator=farmer.scenario_creator, names=lambda S: farmer.scenario_names_creator(1000),
                    kw=lambda S, cm: {"num_scens": 1000, "crops_multiplier": 10}, nodes=None, S=1000,
                    desc="farmer crops_multiplier=10, 1,000 scenarios (BASELINE configs[1])",
@@ -247,7 +299,7 @@ def workloads():
                    kw=lambda S, cm: {"branching_factors": bfs}, S=1000,
                    nodes=sputils.create_nodenames_from_branching_factors(bfs),
                    desc="aircond branching 10x10x10, 1,000 scenarios, 111 non-leaf nodes (BASELINE configs[3])",
-                   cpu=None),
+                   cpu=dict(model="aircond", scens=1000, iters=4, total=1000)),
         "C5a": dict(creator=sslp.scenario_creator, names=lambda S: sslp.scenario_names_creator(10000),
                     kw=lambda S, cm: {"num_scens": 10000}, nodes=None, S=10000,
                     desc="sslp_15_45 LP relaxation, 10,000 stochastic-RHS scenarios (BASELINE configs[4])",
@@ -395,12 +447,14 @@ def dominant_kernel(ph, K, fused):
     return name, ms / 1e3 / max(launches, 1), launches, bpu, units
 
 
-def roofline(kernel, avg_s, launches, bpu, units, traffic=None, traffic_src=None):
+def roofline(kernel, avg_s, launches, bpu, units, traffic=None, traffic_src=None, traffic_status=None):
     bytes_per_launch = bpu * units
     achieved = bytes_per_launch / avg_s / 1e9 if avg_s > 0 else 0.0
     return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/launch",
-            "traffic_source": traffic_src, "algorithmic_bytes_per_launch": bytes_per_launch, "kernel": kernel,
+            "traffic_source": traffic_src, "traffic_status": traffic_status,
+            "traffic_ratio": (traffic / bytes_per_launch) if (traffic and bytes_per_launch) else None,
+            "algorithmic_bytes_per_launch": bytes_per_launch, "kernel": kernel,
             "bytes_per_unit": bpu, "unit_def": "scenario solve", "units_per_launch": units,
             "avg_launch_us": avg_s * 1e6, "launches": launches}
 
@@ -430,8 +484,13 @@ def run_config(name, w, args, K, so, world, dev):
            "solver_options": w.get("so", {})}
     if w.get("cpu") and not args.no_cpu_baseline:
         c = w["cpu"]
-        res["cpu_baseline"] = cpu_baseline(args, model=c["model"], cm=c.get("cm", 1), scens=c["scens"],
-                                           iters=c["iters"], total=c["total"])
+        if c == "headline":
+            # the same subproblems (farmer cm=1) as the headline: its baseline
+            hb = getattr(args, "_headline_cpu", None)
+            res["cpu_baseline"] = dict(hb, note="the headline's (same farmer cm=1 subproblems)") if hb else None
+        else:
+            res["cpu_baseline"] = cpu_baseline(args, model=c["model"], cm=c.get("cm", 1), scens=c["scens"],
+                                               iters=c["iters"], total=c["total"], procs=c.get("procs"))
     del ph
     dev.empty_cache()
     return res
@@ -488,11 +547,12 @@ def main():
     kernel, avg_s, launches, bpu, units = dominant_kernel(ph, K, args.fused)
     b = ph.batch
     if world != 1:
-        traffic, tsrc = None, None
+        traffic, tsrc, tstat = None, None, "N > 1: per-rank PMC not collected"
     elif args.only is not None:
-        traffic, tsrc = pmc_traffic(kernel, CONFIG_PMC_TAG.get(args.only, args.only))
+        traffic, tsrc, tstat = pmc_traffic(kernel, CONFIG_PMC_TAG.get(args.only, args.only))
     else:
-        traffic, tsrc = (pmc_traffic(kernel, "farmer100k") if S == 100000 and cm == 1 else (None, None))
+        traffic, tsrc, tstat = (pmc_traffic(kernel, "farmer100k") if S == 100000 and cm == 1
+                                else (None, None, "no PMC summary for this size"))
     nbad = sum(s.get("not_optimal", 0) for s in ph.solve_stats) + (st.get("not_optimal", 0) if st else 0)
     res = {
         "metric": "PH scenario-iterations/sec (farmer 100k) + time to conv<1e-4",
@@ -514,7 +574,7 @@ def main():
                    "parallelism": "scenario-sharded x%d, RCCL allreduce" % world},
         "T_s": T, "iter0_s": T0,
         "steady": {"value": S * K / Tk, "ms_per_step": Tk * 1e3 / K, "def": "S K / T_iterk (Iter0 excluded)"},
-        "roofline": dict(roofline(kernel, avg_s, launches, bpu, units, traffic, tsrc),
+        "roofline": dict(roofline(kernel, avg_s, launches, bpu, units, traffic, tsrc, tstat),
                          valu=valu_issue(kernel, "farmer100k", units, avg_s)
                          if (world == 1 and args.only is None and S == 100000 and cm == 1) else None),
         "loop": ("PHBase.iterk_loop -> phx_iterk (device-driven, depth %d%s)"
@@ -546,13 +606,16 @@ def main():
         res["allreduce_hook"] = ar_probe(hl, S, cm, args.rho, so, K, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.only is None:
         res["cpu_baseline"] = cpu_baseline(args, cm=cm)
+        args._headline_cpu = res["cpu_baseline"]
     # ---- the other BASELINE configs (one GPU) ----
     if world == 1 and args.only is None and args.configs != "none":
-        names = ["C3x1M", "C2", "C4", "C5a", "C5b"] if args.configs == "all" else args.configs.split(",")
+        names = (["C1", "C3s8", "C3x1M", "C2", "C4", "C5a", "C5b"] if args.configs == "all"
+                 else args.configs.split(","))
         res["configs"] = {}
         for nm in names:
             try:
-                res["configs"][nm] = run_config(nm, W[nm], args, min(K, args.config_steps), so, world, dev)
+                res["configs"][nm] = run_config(nm, W[nm], args, W[nm].get("K", min(K, args.config_steps)), so,
+                                                world, dev)
             except Exception as e:     # reported, never hidden
                 res["configs"][nm] = {"error": repr(e)[:500]}
             print("[bench] %s done" % nm, file=sys.stderr, flush=True)

@@ -262,8 +262,9 @@ PHX_HD double kkt_error(const Prob& P, const double* xs, const double* ys, int s
     const double ep = sqrt(rp2) / (1.0 + sqrt(bn2));
     const double ed = sqrt(rd2) / (1.0 + sqrt(qn2));
     const double eg = fabs(pobj - dobj) / (1.0 + fabs(pobj) + fabs(dobj));
+    // (fmax drops a NaN operand: the sum of the terms catches a non-finite one)
     const double e = fmax(ep, fmax(ed, eg));
-    return isfinite(e) ? e : 1e300;
+    return isfinite(ep + ed + eg) && isfinite(e) ? e : 1e300;
 }
 
 // Restart / primal-weight logic after a chunk; sets St.err[s].
@@ -484,6 +485,7 @@ PHX_HD bool polish_lane(const Prob& P, const State& St, const Polish& W, const O
         double q, p;
         col_cost(P, j, s, q, p);
         const double lam = (q + p * x + atz) / dc;   // y = -z
+        if (!(lam - lam == 0.0)) return false;       // non-finite x or z: no comparison would fail
         if (W.F[o]) {
             if (fabs(lam) > dtol) return false;
         } else if (!(l == u)) {
@@ -499,6 +501,7 @@ PHX_HD bool polish_lane(const Prob& P, const State& St, const Polish& W, const O
             ax += aval(P, k, s) * W.xp[ix(P.colidx[k], s, S)];
         const double dr = P.dr[i];
         const double bl = P.bl.at(i, s), bu = P.bu.at(i, s);
+        if (!(ax - ax == 0.0) || !(W.z[o] - W.z[o] == 0.0)) return false;
         if (ax < bl && (bl - ax) / dr > ptol * (1.0 + fabs(bl / dr))) return false;
         if (ax > bu && (ax - bu) / dr > ptol * (1.0 + fabs(bu / dr))) return false;
         if (W.R[o] && !(bl == bu)) {

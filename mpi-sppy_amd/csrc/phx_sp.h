@@ -435,8 +435,9 @@ PHX_HD double sp_kkt_error(const Prob& P, const SpSym& Y, const SpScr& G, const 
     const double ep = sqrt(acc[0]) / (1.0 + sqrt(acc[1]));
     const double ed = sqrt(acc[2]) / (1.0 + sqrt(acc[3]));
     const double eg = fabs(acc[4] - acc[5]) / (1.0 + fabs(acc[4]) + fabs(acc[5]));
+    // (fmax drops a NaN operand: the sum of the terms catches a non-finite one)
     const double e = fmax(ep, fmax(ed, eg));
-    return isfinite(e) ? e : 1e300;
+    return isfinite(ep + ed + eg) && isfinite(e) ? e : 1e300;
 }
 
 // ---------------------------------------------------------------------------
@@ -801,6 +802,7 @@ PHX_HD int sp_rounds(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds&
                 atz += sp_a(P, Y, P.csc2csr[k], s) * L.yv[P.rowidx[k]];
             const double lam = (G.qq[j] + G.pp[j] * x + atz) / dc;
             G.r1[j] = lam;
+            if (!(lam - lam == 0.0)) bad[0] = 1.0;   // non-finite x or y: no comparison would fail
             const int c = G.cc[j];
             if (c == 0) {
                 if (fabs(lam) > dtol) bad[0] = 1.0;
@@ -814,6 +816,7 @@ PHX_HD int sp_rounds(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds&
             for (int k = P.rowptr[i]; k < P.rowptr[i + 1]; ++k) ax += sp_a(P, Y, k, s) * L.xv[P.colidx[k]];
             G.ax[i] = ax;
             const double dr = P.dr[i], bl = G.bl[i], bu = G.bu[i];
+            if (!(ax - ax == 0.0) || !(L.yv[i] - L.yv[i] == 0.0)) bad[0] = 1.0;
             if (ax < bl && (bl - ax) / dr > ptol * (1.0 + fabs(bl / dr))) bad[0] = 1.0;
             if (ax > bu && (ax - bu) / dr > ptol * (1.0 + fabs(bu / dr))) bad[0] = 1.0;
             if (G.rc[i] && !(bl == bu)) {

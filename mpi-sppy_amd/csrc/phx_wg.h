@@ -529,6 +529,7 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
             for (int k = cp[j]; k < cp[j + 1]; ++k) atz += L.a[c2[k]] * L.z[ri[k]];
             const double lam = (L.qq[j] + L.pp[j] * x + atz) / dc;
             L.r1[j] = lam;
+            if (!(lam - lam == 0.0)) bad = true;   // non-finite x or z: no comparison would fail
             const int8_t c = L.cc[j];
             if (c == 0) {
                 if (fabs(lam) > dtol) bad = true;
@@ -543,6 +544,7 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
             L.u[i] = ax;
             const double dr = P.dr[i];
             const double bl = P.bl.at(i, s), bu = P.bu.at(i, s);
+            if (!(ax - ax == 0.0) || !(L.z[i] - L.z[i] == 0.0)) bad = true;
             if (ax < bl && (bl - ax) / dr > ptol * (1.0 + fabs(bl / dr))) bad = true;
             if (ax > bu && (ax - bu) / dr > ptol * (1.0 + fabs(bu / dr))) bad = true;
             if (L.rc[i] && !(bl == bu)) {

@@ -54,8 +54,19 @@ class PHBase(SPOpt):
         # the device loop's buffers and events, allocated with the problem
         # (phx_iterk_prepare) so no PH iteration pays an allocation
         self._native_comm = False
-        if (self.batch.nonant.N > 0 and self.NNS > 0
-                and self._device_loop_solver(self._solve_opts(self.iterk_solver_options))):
+        # the device loop's solver tier is decided from each rank's own problem;
+        # the ranks must agree (min over the cylinder) before anything
+        # collective depends on it -- the RCCL setup below, phx_iterk's
+        # per-iteration all-reduce -- or ranks that chose differently would wait
+        # on each other forever
+        self._loop_veto = False
+        local = (self.batch.nonant.N > 0 and self.NNS > 0
+                 and self._device_loop_solver(self._solve_opts(self.iterk_solver_options)))
+        agreed = local
+        if self.n_proc > 1:
+            agreed = bool(self.mpicomm.allreduce_np(np.array([1 if local else 0], dtype=np.int64), op="min")[0])
+        self._loop_veto = local and not agreed
+        if agreed:
             if self._want_native_comm():
                 self._setup_native_comm()
             lib = self._native
@@ -334,6 +345,18 @@ class PHBase(SPOpt):
             return False
         if int(o["PHIterLimit"]) < 1:
             return False
+        # a total probability Iter0's check would reject quits before any PH
+        # iteration (phbase.py:812-817): checked here, so a deferred Iter0
+        # never runs iterations first (the same sum the device computes; the
+        # tolerance is far above their rounding difference)
+        E1 = getattr(self, "_E1_pre", None)
+        if E1 is None:        # (host data, once: no device read in the timed Iter0)
+            E1 = float(np.sum(np.asarray(self.batch.prob, dtype=np.float64)))
+            if self.n_proc > 1:
+                E1 = float(self.mpicomm.allreduce_np(np.array([E1]), op="sum")[0])
+            self._E1_pre = E1
+        if abs(1 - E1) > self.E1_tolerance:
+            return False
         saved = self.current_solver_options
         self.current_solver_options = self.options["iterk_solver_options"]
         try:
@@ -499,7 +522,10 @@ class PHBase(SPOpt):
     def _device_loop_solver(self, so):
         """Which solve phx_iterk can run per iteration: the lane solver (jit on),
         or, above its size limits, the workgroup warm pass (k_wg_warm), or above
-        those the sparse solver's warm pass (k_sp_solve)."""
+        those the sparse solver's warm pass (k_sp_solve).  False on every rank
+        when some rank of the cylinder cannot (_loop_veto, set at construction)."""
+        if getattr(self, "_loop_veto", False):
+            return False
         info = getattr(self, "_jit_info", None)
         if info is None:
             info = self._jit_info = self._native.jit_info(self._ctx).decode()

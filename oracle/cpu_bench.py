@@ -31,8 +31,14 @@ if _ROOT not in sys.path:
 from oracle import models as om, ph as oph  # noqa: E402
 
 
+AIRCOND_BF = [10, 10, 10]       # C4 (BASELINE configs[3])
+
+
 def make_scen(model, nm, S, cm=1):
-    """One oracle scenario of the bench workloads (two-stage: one ROOT x-bar)."""
+    """One oracle scenario of the bench workloads (two-stage: one ROOT x-bar;
+    aircond: the multistage tree of C4, x-bar per tree node)."""
+    if model == "aircond":
+        return om.aircond(nm, AIRCOND_BF)
     if model == "farmer":
         return om.farmer(nm, crops_multiplier=cm, num_scens=S)
     if model == "sslp":
@@ -43,7 +49,7 @@ def make_scen(model, nm, S, cm=1):
 
 
 def names_of(model, S):
-    if model == "farmer":
+    if model in ("farmer", "aircond"):
         return ["scen%d" % i for i in range(S)]
     if model == "sslp":
         return ["Scenario%d" % (i + 1) for i in range(S)]
@@ -68,22 +74,41 @@ def fast_solver(scens):
     return solve
 
 
+def _node_partials(o):
+    """The worker's share of _Compute_Xbar's per-node sums (phbase.py:54-80):
+    {(node, slot): [sum pc x, sum pc x^2]} over its scenarios (multistage)."""
+    xn = o.xn()
+    part = {}
+    for k in range(o.S):
+        for j in range(o.N):
+            a = part.setdefault((o.node_of[k][j], j), [0.0, 0.0])
+            v = o.pc[k, j] * xn[k, j]
+            a[0] += v
+            a[1] += v * xn[k, j]
+    return part
+
+
 def _worker(conn, names, S, cm, rho, model="farmer"):
     scens = [make_scen(model, nm, S, cm) for nm in names]
     o = oph.OraclePH(scens, rho=rho)
     o.solver = fast_solver(scens)
     o.iter0()
-    conn.send((o.xn(), o.obj.copy()))
+    multi = model == "aircond"
+    conn.send((_node_partials(o) if multi else o.xn(), o.obj.copy()))
     while True:
         msg = conn.recv()
         if msg is None:
             break
-        xbar = msg
-        o.xbar[:] = xbar[None, :]
+        if multi:      # the all-reduced node sums: x-bar per (node, slot)
+            for k in range(o.S):
+                for j in range(o.N):
+                    o.xbar[k, j] = msg[(o.node_of[k][j], j)]
+        else:
+            o.xbar[:] = msg[None, :]
         o.update_w()
         d = float(np.sum(np.abs(o.xn() - o.xbar)))
         o.solve_loop()
-        conn.send((o.xn(), d))
+        conn.send((_node_partials(o) if multi else o.xn(), d))
     conn.close()
 
 
@@ -105,17 +130,29 @@ def run(S, K, P, cm=1, rho=1.0, model="farmer", S_total=None):
         procs.append(p)
     res = [c.recv() for c in pipes]          # Iter0 done everywhere
     t_setup = time.perf_counter() - t_setup
+    multi = model == "aircond"
     prob = 1.0 / S                           # x-bar over the sample
-    xn = np.concatenate([r[0] for r in res])
     t0 = time.perf_counter()
     conv = None
     for _ in range(K):
-        xbar = prob * xn.sum(axis=0)         # Compute_Xbar (+ the Allreduce)
+        if multi:
+            # the per-node Allreduce (phbase.py:83-87): the full tree is run
+            tot = {}
+            for r in res:
+                for key, (a, b) in r[0].items():
+                    t = tot.setdefault(key, [0.0, 0.0])
+                    t[0] += a
+                    t[1] += b
+            xbar = {key: v[0] for key, v in tot.items()}
+            nslot = 1 + max(j for (_, j) in tot)
+        else:
+            xn = np.concatenate([r[0] for r in res])
+            xbar = prob * xn.sum(axis=0)     # Compute_Xbar (+ the Allreduce)
+            nslot = xn.shape[1]
         for c in pipes:
             c.send(xbar)
         res = [c.recv() for c in pipes]
-        xn = np.concatenate([r[0] for r in res])
-        conv = sum(r[1] for r in res) / (S * xn.shape[1])
+        conv = sum(r[1] for r in res) / (S * nslot)
     dt = time.perf_counter() - t0
     for c in pipes:
         c.send(None)
@@ -126,23 +163,41 @@ def run(S, K, P, cm=1, rho=1.0, model="farmer", S_total=None):
             "sample": "oracle PH restatement (numpy + persistent scipy-HiGHS 1.8 LP/QP + one KKT polish of its basis; "
                       "sparse IPM + certified polish above 300 rows+cols), %s, %d scenarios x %d PH iterations "
                       "after Iter0, %d worker processes (contiguous slices, parent = Allreduce)"
-                      % ("farmer cm=%d" % cm if model == "farmer" else model, S, K, P),
+                      % ("farmer cm=%d" % cm if model == "farmer" else
+                         ("aircond %s (the whole tree, per-node x-bar)" % "x".join(map(str, AIRCOND_BF))
+                          if model == "aircond" else model), S, K, P),
             "host": host_info()}
 
 
 def host_info():
-    """nproc and the CPU model of the machine the baseline ran on."""
+    """nproc, physical cores / sockets (distinct (physical id, core id) pairs of
+    /proc/cpuinfo: lscpu's cores x sockets) and the CPU model of the machine
+    the baseline ran on."""
     model = None
+    cores, sockets, phys, core = set(), set(), None, None
     try:
         with open("/proc/cpuinfo") as f:
             for line in f:
-                if line.startswith("model name"):
-                    model = line.split(":", 1)[1].strip()
-                    break
+                k, _, v = line.partition(":")
+                k, v = k.strip(), v.strip()
+                if k == "model name" and model is None:
+                    model = v
+                elif k == "physical id":
+                    phys = v
+                    sockets.add(v)
+                elif k == "core id":
+                    core = v
+                elif not k:
+                    if phys is not None and core is not None:
+                        cores.add((phys, core))
+                    phys = core = None
+        if phys is not None and core is not None:
+            cores.add((phys, core))
     except OSError:
         pass
     aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None
-    return {"nproc": os.cpu_count(), "affinity_cpus": aff, "cpu_model": model}
+    return {"nproc": os.cpu_count(), "affinity_cpus": aff, "cpu_model": model,
+            "physical_cores": len(cores) or None, "sockets": len(sockets) or None}
 
 
 def main():
@@ -152,7 +207,7 @@ def main():
     ap.add_argument("--procs", type=int, default=min(16, os.cpu_count() or 1))
     ap.add_argument("--cm", type=int, default=1)
     ap.add_argument("--rho", type=float, default=1.0)
-    ap.add_argument("--model", default="farmer", choices=["farmer", "sslp", "netdes50"])
+    ap.add_argument("--model", default="farmer", choices=["farmer", "sslp", "netdes50", "aircond"])
     ap.add_argument("--scens-total", type=int, default=None, help="probability 1/S_total (the full workload)")
     a = ap.parse_args()
     print(json.dumps(run(a.scens, a.iters, a.procs, a.cm, a.rho, a.model, a.scens_total)), flush=True)

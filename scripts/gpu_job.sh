@@ -40,7 +40,9 @@ for step in "$@"; do
       tag="${rest%%:*}"; rest2="${rest#*:}"; ctr="${rest2%%:*}"; args="${rest2#*:}"; log="gpurun_out/${tag}.log"
       echo "== step $n: rocprofv3 --pmc ${ctr//,/ } bench.py $args"
       timeout -s KILL 240 rocprofv3 --pmc ${ctr//,/ } -d "gpurun_out/${tag}" -o run -- python3 bench.py $args > "$log" 2>&1
-      rc=$?; tail -2 "$log" ;;
+      rc=$?; tail -2 "$log"
+      # the sources this pass measured (scripts/pmc_summary.py records it)
+      python3 scripts/src_hash.py > "gpurun_out/${tag}/src_hash.json" ;;
     py)
       tag="${rest%%:*}"; args="${rest#*:}"; log="gpurun_out/${tag}.log"
       echo "== step $n: python $args"

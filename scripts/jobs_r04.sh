@@ -1,0 +1,19 @@
+#!/bin/bash
+# Round-4 GPU evidence jobs (run through gpurun): bash scripts/jobs_r04.sh <name>.
+# Each job is a list of scripts/gpu_job.sh steps; logs land in gpurun_out/, the
+# summaries judged are copied into profiles/ (named after the job).
+set -o pipefail
+B="--configs none --no-cpu-baseline --no-conv --steps 50"                 # headline, K = 50
+H="--configs none --no-cpu-baseline --no-conv"                            # headline, K = 20 (driver shape)
+M="--configs none --no-cpu-baseline --no-conv --steps 20 --warmup 1 --scens 1000000 --ar-probe 0"   # over-cache 1M
+A="--no-cpu-baseline --no-conv --steps 10 --warmup 1"                     # one secondary config
+S8="--only C3s8 --no-cpu-baseline --no-conv --steps 20"                   # the 8-GPU per-rank slice
+SQ="SQ_INSTS_VALU,SQ_ACTIVE_INST_VALU,SQ_WAVE_CYCLES,SQ_WAIT_ANY,SQ_INSTS_VALU_FLOPS_FP64,SQ_INSTS_SALU"
+J="bash scripts/gpu_job.sh"
+case "$1" in
+  s1)  $J "bench:r04_s1_c3s8:$S8" "prof:r04_s1_c3s8_prof:$S8" "prof:r04_s1_prof:$H --ar-probe 0" && \
+       PHX_LANE_STAMPS=1 $J "bench:r04_s1_c3s8_stamps:$S8" ;;
+  s2)  $J "test:tests" "bench:r04_s2_c3s8:$S8" "bench:r04_s2_bench:$H" "prof:r04_s2_c3s8_prof:$S8" && \
+       PHX_LANE_DEFS=PHX_RELAXED_HANDOFF $J "bench:r04_s2_bench_relaxed:$H" "bench:r04_s2_c3s8_relaxed:$S8" ;;
+  *) echo "unknown job $1"; exit 2 ;;
+esac

@@ -43,6 +43,7 @@ def main(kernel, dirs, last=None):
                 if base_name(name) == kernel:
                     agg[ctr][int(disp)] += float(val)
             add(agg, out, last)
+    provenance(out, dirs)
     finish(out)
 
 
@@ -59,6 +60,24 @@ def add(agg, out, last):
             v = v[-last:]
         out["counters"][k] = sum(v) / len(v)
         out["launches"][k] = len(v)
+
+
+def provenance(out, dirs):
+    """The sources the passes measured (src_hash.json written next to each pass
+    by scripts/gpu_job.sh on the GPU box) and the git head this summary was
+    made at: bench.py uses a summary only while its kernel's sources hash the same."""
+    import subprocess
+    shas = set()
+    for d in dirs:
+        for f in glob.glob(os.path.join(d, "**", "src_hash.json"), recursive=True):
+            shas.add(json.load(open(f)).get(out["kernel"]))
+    out["source_sha256"] = shas.pop() if len(shas) == 1 else (None if not shas else "mixed")
+    try:
+        head = subprocess.run(["git", "rev-parse", "HEAD"], capture_output=True, text=True,
+                              cwd=os.path.dirname(os.path.abspath(__file__))).stdout.strip()
+    except OSError:
+        head = None
+    out["git_head_at_summary"] = head or None
 
 
 def finish(out):

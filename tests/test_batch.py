@@ -24,12 +24,24 @@ def _same(a, b):
     assert a.nonant.var_names == b.nonant.var_names
 
 
-@pytest.mark.parametrize("cm", [1, 2, 11])
+# 40 and 110: the vectorised yields draw 6 cm words per scenario, past the 227
+# of the first half-twist (40) and past one whole 624-word twist (110)
+@pytest.mark.parametrize("cm", [1, 2, 11, 40, 110])
 def test_farmer_batch_equals_models(cm):
     names = farmer.scenario_names_creator(20)
     kw = {"crops_multiplier": cm, "num_scens": 20}
     models = [farmer.scenario_creator(n, **kw) for n in names]
     _same(farmer.batch_creator(names, **kw), bm.from_models(names, models))
+
+
+@pytest.mark.parametrize("k", [1, 227, 228, 623, 624, 625, 1300])
+def test_rng_first_rands_any_length(k):
+    """utils/rng.py against numpy's own legacy RandomState, across twist boundaries."""
+    from mpisppy_amd.utils import rng
+    seeds = np.array([0, 1, 7, 12345, 2 ** 32 - 1])
+    got = rng.first_rands(seeds, k)
+    for i, sd in enumerate(seeds):
+        assert np.array_equal(got[i], np.random.RandomState(int(sd)).rand(k))
 
 
 def test_farmer_nonant_order_string_sort():

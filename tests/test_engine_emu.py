@@ -7,7 +7,8 @@ import os
 import numpy as np
 import pytest
 
-from helpers import all_certified, oracle_continue_from, REF_W, REF_XBAR, rel, run_engine
+from helpers import all_certified, oracle_continue_from, ph_options, REF_W, REF_XBAR, rel, run_engine
+from mpisppy_amd.opt.ph import PH
 from mpisppy_amd.examples import aircond, farmer
 from mpisppy_amd.utils import sputils
 from oracle import models as om, ph as oph
@@ -399,3 +400,65 @@ def test_deferred_iter0_emu(emu, so0):
     a, b = check_deferred_iter0(emu, "cpu", iter0_solver=so0)
     if so0:
         assert a.solve_stats[0]["stragglers"] > 0      # Iter0's leftovers finished after adoption
+
+
+def infeasible_farmer_creator(sname, **kw):
+    """farmer, except scen1 must plant 400 + 400 acres of wheat and corn on a
+    500-acre farm: its Iter0 LP is infeasible."""
+    m = farmer.scenario_creator(sname, **kw)
+    if sname == "scen1":
+        m.DevotedAcreage["WHEAT0"].lb = 400.0
+        m.DevotedAcreage["CORN0"].lb = 400.0
+    return m
+
+
+def check_infeasible_deferred_iter0(lib, device, S=30):
+    """ph_main defers Iter0's checks to the device loop; an Iter0 with an
+    infeasible scenario still quits before any PH iteration runs, as the
+    reference does right after Iter0 (phbase.py:812-823): phx_iterk stops
+    after adopting that solve (no iteration ran) and the checks quit()."""
+    ph = PH(ph_options(20), farmer.scenario_names_creator(S), infeasible_farmer_creator,
+            scenario_creator_kwargs={"num_scens": S}, _native_lib=lib, _device=device)
+    seen = []
+    orig = ph._native.iterk
+
+    def spy(ctx, so, a, res, stream):
+        rc = orig(ctx, so, a, res, stream)
+        seen.append((res._obj.iters, res._obj.solves, res._obj.adopted))
+        return rc
+    ph._native.iterk = spy
+    with pytest.raises(SystemExit):
+        ph.ph_main()
+    ph._native.iterk = orig
+    assert seen == [(0, 0, 1)], seen          # adopted Iter0, no PH iteration
+    assert ph.E1 == pytest.approx(1.0)
+
+
+def test_infeasible_deferred_iter0_emu(emu):
+    check_infeasible_deferred_iter0(emu, "cpu")
+
+
+def check_infeasible_iter0_status(lib, device, S=30):
+    """The infeasible scenario is never certified (its lane-solver refinement
+    diverges to a non-finite point, which every KKT certificate must reject --
+    before round 4 a NaN point passed them all and was reported OPTIMAL): it
+    ends without an optimal status (here the generic path's iteration limit:
+    its interior point finds no Farkas certificate with margin for this
+    instance) while every other scenario is optimal and finite, and Iter0's
+    feasibility check quits (phbase.py:818-823)."""
+    ph = PH(ph_options(0), farmer.scenario_names_creator(S), infeasible_farmer_creator,
+            scenario_creator_kwargs={"num_scens": S}, _native_lib=lib, _device=device)
+    ph.PH_Prep()
+    ph.subproblem_creation(False)
+    with pytest.raises(SystemExit):
+        ph.Iter0()
+    st = ph._status.cpu().numpy()
+    assert st[1] != 1, st[:4]
+    assert (np.delete(st, 1) == 1).all()
+    x = ph._host("x")
+    assert np.isfinite(np.delete(x, 1, axis=1)).all()
+    assert ph.solve_stats[-1]["not_optimal"] == 1
+
+
+def test_infeasible_iter0_status_emu(emu):
+    check_infeasible_iter0_status(emu, "cpu")

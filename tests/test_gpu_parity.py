@@ -348,16 +348,54 @@ def test_time_to_conv_gpu(gpu_lib, S):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("variant", ["PHX_FENCED_HANDOFF", "PHX_RELAXED_HANDOFF"])
 @pytest.mark.parametrize("S", [1000, 20000])
-def test_fenced_handoff_fused_loop_gpu(gpu_lib, monkeypatch, S):
-    """The fused loop's inter-workgroup hand-off with agent-scope release/acquire
-    fences (PHX_FENCED_HANDOFF, phx_lane.h) gives the host loop's trajectory,
-    as the default relaxed write-through hand-off does; at 20k scenarios (79
-    workgroups) every arrival shard and the top counter are used."""
-    monkeypatch.setenv("PHX_LANE_DEFS", "PHX_FENCED_HANDOFF")
+def test_handoff_variants_fused_loop_gpu(gpu_lib, monkeypatch, S, variant):
+    """The fused loop's inter-workgroup hand-off in its two opt-in variants --
+    release fences on the producers too (PHX_FENCED_HANDOFF), or no acquire on
+    the consumers (PHX_RELAXED_HANDOFF: `sc1` loads alone) -- gives the host
+    loop's trajectory, as the default (write-through producers, acquiring
+    consumers; phx_lane.h) does; at 20k scenarios (79 workgroups) every arrival
+    shard and the top counter are used."""
+    monkeypatch.setenv("PHX_LANE_DEFS", variant)
     from test_engine_emu import check_native_vs_host
     a, b = check_native_vs_host(gpu_lib, None, "farmer", S=S, fused=1)
     assert a.iterk_stats["fused"]
+
+
+@pytest.mark.gpu
+def test_infeasible_iter0_status_gpu(gpu_lib):
+    from test_engine_emu import check_infeasible_iter0_status
+    check_infeasible_iter0_status(gpu_lib, None)
+
+
+@pytest.mark.gpu
+def test_infeasible_deferred_iter0_gpu(gpu_lib):
+    from test_engine_emu import check_infeasible_deferred_iter0
+    check_infeasible_deferred_iter0(gpu_lib, None)
+
+
+@pytest.mark.gpu
+def test_unseeded_and_seeded_iter0_agree_gpu(gpu_lib, monkeypatch):
+    """Iter0 seeds from templates only when the batch has more wavefronts than
+    SIMDs (phx_solve); both routes certify every lane at the same optimum
+    (PHX_FORCE_SEED takes the seeded route at 20k scenarios)."""
+    import torch
+    S = 20000
+    runs = []
+    for force in (False, True):
+        if force:
+            monkeypatch.setenv("PHX_FORCE_SEED", "1")
+        ph = PH(ph_options(0), farmer.scenario_names_creator(S), farmer.scenario_creator,
+                scenario_creator_kwargs={"num_scens": S}, _native_lib=gpu_lib)
+        conv, Eobj, tb = ph.ph_main()
+        runs.append((ph._obj.cpu().numpy().copy(), tb, ph._status.cpu().numpy().copy()))
+        del ph
+        torch.cuda.empty_cache()
+    (o0, tb0, s0), (o1, tb1, s1) = runs
+    assert (s0 == 1).all() and (s1 == 1).all()
+    assert rel(o0, o1) < 1e-9
+    assert abs(tb0 - tb1) <= 1e-9 * abs(tb0)
 
 
 @pytest.mark.gpu
