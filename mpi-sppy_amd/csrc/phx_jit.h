@@ -33,6 +33,10 @@ struct LaneStructure {
     std::vector<int32_t> row, col, kvar, col_slot;
     std::vector<int32_t> pair_a, pair_b, pair_pos;
     std::vector<uint8_t> lnz;   // packed lower triangle: structurally nonzero in L (pairs + fill)
+    // entry k is the first of its row / of its column in CSR order; rows /
+    // columns without entries (the mat-vecs start from the first product
+    // instead of adding it to 0.0, which IEEE arithmetic keeps as an add)
+    std::vector<uint8_t> rfirst, cfirst, rempty, cempty;
     std::vector<uint8_t> lfin, ufin, fixed, blfin, bufin, eq;
     // scenario-invariant numbers (scaled iff `scaled`), baked into the kernel
     // as literals (c / lb,ub / bl,bu only when they do not vary across
@@ -77,6 +81,12 @@ inline bool build_lane_structure(const HostSetup& hs, int n, int m, int nnz, boo
     L.col_slot.assign(hs.col_slot.begin(), hs.col_slot.end());
     L.nvar = 0;
     for (int k = 0; k < nnz; ++k) L.nvar = std::max(L.nvar, hs.kvar[k] + 1);
+    L.rfirst.assign(nnz, 0); L.cfirst.assign(nnz, 0); L.rempty.assign(m, 1); L.cempty.assign(n, 1);
+    for (int k = 0; k < nnz; ++k) {
+        const int i = hs.rowof[k], j = hs.colidx[k];
+        if (L.rempty[i]) { L.rfirst[k] = 1; L.rempty[i] = 0; }
+        if (L.cempty[j]) { L.cfirst[k] = 1; L.cempty[j] = 0; }
+    }
     L.nslot = (int)hs.slot_col.size();
     L.pair_a.clear(); L.pair_b.clear(); L.pair_pos.clear();
     for (int j = 0; j < n; ++j)
@@ -183,6 +193,10 @@ inline std::string lane_kernel_source(const LaneStructure& L, int warm_waves = 1
     emit_table(o, "int", "pair_b", L.pair_b);
     emit_table(o, "int", "pair_pos", L.pair_pos);
     emit_table(o, "bool", "lnz", L.lnz);
+    emit_table(o, "bool", "rfirst", L.rfirst);
+    emit_table(o, "bool", "cfirst", L.cfirst);
+    emit_table(o, "bool", "rempty", L.rempty);
+    emit_table(o, "bool", "cempty", L.cempty);
     emit_table(o, "bool", "lfin", L.lfin);
     emit_table(o, "bool", "ufin", L.ufin);
     emit_table(o, "bool", "fixed", L.fixed);

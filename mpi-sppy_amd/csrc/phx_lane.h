@@ -70,6 +70,9 @@ typedef unsigned long long uint64_t;
 #ifndef PHX_LANE_STAT
 #define PHX_LANE_STAT(kind)
 #endif
+#ifndef PHX_REFINE_HOOK
+#define PHX_REFINE_HOOK(step, d2, tol2)
+#endif
 
 namespace phx_lane {
 
@@ -226,24 +229,35 @@ struct Data {
     double qn[PT::NMAX_S], pn[PT::NMAX_S];
     double kn;
 
+    // Every load is unconditional and issued before any is used (the lane
+    // kernels run one wavefront per SIMD at small batches, so each dependent
+    // memory round trip is paid in full): the PH-term switches select values
+    // instead of guarding loads -- guarded, each slot's loads sat in a branch
+    // of their own behind the previous slot's wait, ~6 serial L2 round trips
+    // per construction (ISA, r04).  The arrays are always readable: lane_io
+    // substitutes zero arrays of the full size for absent ones.
     PHX_LD Data(const LaneIO& io_, int sc_) : io(io_), sc(sc_) {
         const int S = io.S;
+        double wv[PT::NMAX_S], rv[PT::NMAX_S];
+        int32_t xi[PT::NMAX_S];
         PHX_UNROLL for (int v = 0; v < PT::nvar(); ++v) av[v] = io.Av[(int64_t)v * S + sc];
-        kn = 0.0;
         PHX_UNROLL for (int t = 0; t < PT::nslot(); ++t) {
             const int64_t o = (int64_t)t * S + sc;
-            double q = 0.0, p = 0.0;
-            if (io.W_on) q = io.W[o];
-            if (io.prox_on) {
-                // fused mode (one tree node, node slot = nonant slot): x-bar of
-                // slot t is stage[t], no index gather
-                const double r = io.rho[o], xb = io.xbar_node[io.fz.on ? t : io.xbar_idx[o]];
-                q -= r * xb;
-                p = r;
-                kn += 0.5 * r * xb * xb;
-            }
-            qn[t] = q;
-            pn[t] = p;
+            wv[t] = io.W[o];
+            rv[t] = io.rho[o];
+            xi[t] = io.xbar_idx[o];
+        }
+        const bool won = io.W_on != 0, pon = io.prox_on != 0, fzon = io.fz.on != 0;
+        kn = 0.0;
+        PHX_UNROLL for (int t = 0; t < PT::nslot(); ++t) {
+            // fused mode (one tree node, node slot = nonant slot): x-bar of
+            // slot t is stage[t], no index gather
+            const double xb = io.xbar_node[fzon ? t : xi[t]];
+            const double r = pon ? rv[t] : 0.0;
+            const double w = won ? wv[t] : 0.0;
+            qn[t] = w - r * xb;
+            pn[t] = r;
+            kn += 0.5 * r * xb * xb;
         }
     }
     PHX_LD double A(int k) const { return PT::kvar(k) < 0 ? PT::Ac(k) : av[PT::kvar(k)]; }
@@ -264,14 +278,25 @@ struct Data {
     PHX_LD double bl(int i) const { return PT::rhs_vary() ? io.bl[(int64_t)i * io.S + sc] : PT::bls(i); }
     PHX_LD double bu(int i) const { return PT::rhs_vary() ? io.bu[(int64_t)i * io.S + sc] : PT::bus(i); }
 
+    // (each row / column sum starts from its first product: 0.0 + v is an
+    // add IEEE arithmetic keeps, one per row and column per mat-vec)
     PHX_LD void matvec(const double* xv, double* ax) const {
-        PHX_UNROLL for (int i = 0; i < PT::m(); ++i) ax[i] = 0.0;
-        PHX_UNROLL for (int k = 0; k < PT::nnz(); ++k) ax[PT::row(k)] += A(k) * xv[PT::col(k)];
+        PHX_UNROLL for (int i = 0; i < PT::m(); ++i) if (PT::rempty(i)) ax[i] = 0.0;
+        PHX_UNROLL for (int k = 0; k < PT::nnz(); ++k) {
+            const double v = A(k) * xv[PT::col(k)];
+            ax[PT::row(k)] = PT::rfirst(k) ? v : ax[PT::row(k)] + v;
+        }
     }
     PHX_LD void matvec_t(const double* yv, double* aty) const {
-        PHX_UNROLL for (int j = 0; j < PT::n(); ++j) aty[j] = 0.0;
-        PHX_UNROLL for (int k = 0; k < PT::nnz(); ++k) aty[PT::col(k)] += A(k) * yv[PT::row(k)];
+        PHX_UNROLL for (int j = 0; j < PT::n(); ++j) if (PT::cempty(j)) aty[j] = 0.0;
+        PHX_UNROLL for (int k = 0; k < PT::nnz(); ++k) {
+            const double v = A(k) * yv[PT::row(k)];
+            aty[PT::col(k)] = PT::cfirst(k) ? v : aty[PT::col(k)] + v;
+        }
     }
+    // q_j + p_j x: the prox term's gradient exists on the nonant columns only
+    // (p_j = 0 elsewhere: no 0 * x, which IEEE arithmetic keeps)
+    PHX_LD double qpx(int j, double x) const { return PT::col_slot(j) >= 0 ? q(j) + p(j) * x : q(j); }
 
     // relative KKT error, unscaled measure (phx_core.h kkt_error)
     PHX_LD double kkt(const double* xv, const double* yv) const {
@@ -296,15 +321,16 @@ struct Data {
         matvec_t(yv, aty);
         PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
             const double qj = q(j), pj = p(j), d = dc(j);
-            const double lam_s = qj + pj * xv[j] - aty[j];
+            const bool ps = PT::col_slot(j) >= 0;          // (p_j = 0 off the nonant columns)
+            const double lam_s = qpx(j, xv[j]) - aty[j];
             const double lam = lam_s / d;
             double rd = lam;
             if (PT::lfin(j) && lam > 0.0) { rd = 0.0; dobj += l(j) * lam_s; }
             if (PT::ufin(j) && lam < 0.0) { rd = 0.0; dobj += u(j) * lam_s; }
             rd2 += rd * rd;
             qn2 += (qj / d) * (qj / d);
-            pobj += qj * xv[j] + 0.5 * pj * xv[j] * xv[j];
-            dobj -= 0.5 * pj * xv[j] * xv[j];
+            pobj += ps ? qj * xv[j] + 0.5 * pj * xv[j] * xv[j] : qj * xv[j];
+            if (ps) dobj -= 0.5 * pj * xv[j] * xv[j];
         }
         const double ep = sqrt(rp2) / (1.0 + sqrt(bn2));
         const double ed = sqrt(rd2) / (1.0 + sqrt(qn2));
@@ -741,6 +767,35 @@ struct ASet {
     PHX_LD void setLo(int i, bool v) { l = v ? (l | (1u << i)) : (l & ~(1u << i)); }
 };
 
+// A lane's boolean as a 0/1 integer in a vector register.  Every per-lane
+// bool is a 64-bit lane mask in scalar registers; the ~40 an active set and
+// its certificate keep live spilled to VGPR lanes (v_writelane / v_readlane,
+// ~500 of them in the r03 warm kernel).  The empty asm keeps the compiler from
+// folding the 0/1 values back into lane-mask logic.
+PHX_LD uint32_t vbit(bool b) {
+    uint32_t v = b ? 1u : 0u;
+#if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC_RTC__)
+    __asm__ volatile("" : "+v"(v));
+#endif
+    return v;
+}
+// bit k of an active-set word as a 0/1 double (a multiplier)
+template <class W>
+PHX_LD double bitd(W w, int k) { return (double)(uint32_t)((w >> k) & 1u); }
+
+// An active set's bits as multipliers, once per round: the factor and the
+// refinement scale by them instead of selecting (x * 1 and x + (+-0) are exact,
+// so the factor and the iterates are bit for bit those of the selecting code).
+template <class PT>
+struct AMul {
+    double fF[PT::NMAX_N];   // 1: column free
+    double rR[PT::NMAX_M];   // 1: row active
+    PHX_LD explicit AMul(const ASet<PT>& a) {
+        PHX_UNROLL for (int j = 0; j < PT::n(); ++j) fF[j] = bitd(a.f, j);
+        PHX_UNROLL for (int i = 0; i < PT::m(); ++i) rR[i] = bitd(a.r, i);
+    }
+};
+
 template <class PT>
 PHX_LD void aset_load(const LaneIO& io, int sc, ASet<PT>& a) {
     constexpr int NW = aset_words(PT::NMAX_N, PT::NMAX_M);
@@ -791,7 +846,7 @@ PHX_LD void classify(const Data<PT>& D, const double* xv, const double* yv, doub
     double aty[PT::NMAX_N];
     D.matvec_t(yv, aty);
     PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
-        const double lam = D.q(j) + D.p(j) * xv[j] - aty[j];
+        const double lam = D.qpx(j, xv[j]) - aty[j];
         bool fr = !PT::fixed(j), upj = false;
         if (fr && PT::lfin(j)) {
             const double lo = D.l(j);
@@ -839,19 +894,24 @@ struct KFactor {
 };
 
 template <class PT>
-PHX_LD bool kkt_factor(const Data<PT>& D, const ASet<PT>& a, KFactor<PT>& K) {
+PHX_LD bool kkt_factor(const Data<PT>& D, const AMul<PT>& am, KFactor<PT>& K) {
     constexpr int TT = PT::NMAX_M * (PT::NMAX_M + 1) / 2;
     constexpr double reg = KKT_REG;
     // 1/(p_j + reg): a literal for columns without a PH slot (p = 0), three
-    // or so reciprocals for the nonant columns; masked by F(j) where needed
+    // or so reciprocals for the nonant columns
     PHX_UNROLL for (int j = 0; j < PT::n(); ++j)
         if (PT::col_slot(j) >= 0) K.ipn[PT::col_slot(j)] = 1.0 / (D.p(j) + reg);
     PHX_UNROLL for (int t = 0; t < TT; ++t) K.M[t] = 0.0;
-    PHX_UNROLL for (int i = 0; i < PT::m(); ++i) K.M[tri(i, i)] = a.R(i) ? reg : 1.0;
+    // active rows reg, inactive 1: rR reg + (1 - rR), exact for rR in {0, 1}
+    PHX_UNROLL for (int i = 0; i < PT::m(); ++i) K.M[tri(i, i)] = fma(am.rR[i], reg, 1.0 - am.rR[i]);
+    // A's entries of inactive rows and H^-1 of non-free columns as zeros:
+    // (gA_a h) gA_b is A_a H^-1 A_b when both rows are active and the column is
+    // free, an exact zero otherwise
+    double gA[PT::NMAX_K > 0 ? PT::NMAX_K : 1];
+    PHX_UNROLL for (int k = 0; k < PT::nnz(); ++k) gA[k] = D.A(k) * am.rR[PT::row(k)];
     PHX_UNROLL for (int t = 0; t < PT::npairs(); ++t) {
-        const int ka = PT::pair_a(t), kb = PT::pair_b(t);
-        if (a.R(PT::row(ka)) && a.R(PT::row(kb)) && a.F(PT::col(ka)))
-            K.M[PT::pair_pos(t)] += D.A(ka) * K.Hinv(PT::col(ka)) * D.A(kb);
+        const int ka = PT::pair_a(t), kb = PT::pair_b(t), j = PT::col(ka);
+        K.M[PT::pair_pos(t)] += gA[ka] * (K.Hinv(j) * am.fF[j]) * gA[kb];
     }
     if (!cholesky<PT>(K.M)) { PHX_LANE_FAIL(10, -1); return false; }
     return true;
@@ -863,32 +923,35 @@ PHX_LD bool kkt_factor(const Data<PT>& D, const ASet<PT>& a, KFactor<PT>& K) {
 // proximal-point iteration: it converges to the solution nearest the start on
 // degenerate faces).
 template <class PT, class RHS>
-PHX_LD void kkt_refine(const Data<PT>& D, const ASet<PT>& a, const KFactor<PT>& K, const RHS& R, double* xp,
+PHX_LD void kkt_refine(const Data<PT>& D, const AMul<PT>& am, const KFactor<PT>& K, const RHS& R, double* xp,
                        double* z) {
     constexpr int NN = PT::NMAX_N, MM = PT::NMAX_M;
-    PHX_UNROLL for (int j = 0; j < PT::n(); ++j)
-        if (!a.F(j)) xp[j] = R.xb(j);
-    PHX_UNROLL for (int i = 0; i < PT::m(); ++i) if (!a.R(i)) z[i] = 0.0;
+    PHX_UNROLL for (int j = 0; j < PT::n(); ++j) xp[j] = am.fF[j] != 0.0 ? xp[j] : R.xb(j);
+    PHX_UNROLL for (int i = 0; i < PT::m(); ++i) z[i] *= am.rR[i];
     // the free columns as a multiplier, once: hf = H^-1 on free columns and 0
     // elsewhere; the column loops then run without selects (non-free
     // components get exact zero corrections, so xp keeps its bound values bit
-    // for bit)
-    double hf[NN];
-    PHX_UNROLL for (int j = 0; j < PT::n(); ++j) hf[j] = a.F(j) ? K.Hinv(j) : 0.0;
+    // for bit); the active rows' right-hand sides (finite: R.b's finite side)
+    double hf[NN], bR[MM];
+    PHX_UNROLL for (int j = 0; j < PT::n(); ++j) hf[j] = am.fF[j] * K.Hinv(j);
+    PHX_UNROLL for (int i = 0; i < PT::m(); ++i) bR[i] = R.b(i);
+#ifdef PHX_REFINE_PREDICT
+    double dprev2 = 1e300;
+#endif
     PHX_REFINE_LOOP for (int it = 0; it < KKT_REFINE; ++it) {
         double g[NN], t[MM];
         {
             double atz[NN];
             D.matvec_t(z, atz);
-            PHX_UNROLL for (int j = 0; j < PT::n(); ++j) g[j] = -R.q(j) - D.p(j) * xp[j] - atz[j];
+            PHX_UNROLL for (int j = 0; j < PT::n(); ++j)
+                g[j] = (PT::col_slot(j) >= 0 ? -R.q(j) - D.p(j) * xp[j] : -R.q(j)) - atz[j];
         }
         {
             double axp[MM], hr[NN], ahr[MM];
             D.matvec(xp, axp);
             PHX_UNROLL for (int j = 0; j < PT::n(); ++j) hr[j] = g[j] * hf[j];
             D.matvec(hr, ahr);
-            // (a select: the inactive side of a row may be infinite)
-            PHX_UNROLL for (int i = 0; i < PT::m(); ++i) t[i] = a.R(i) ? ahr[i] - (R.b(i) - axp[i]) : 0.0;
+            PHX_UNROLL for (int i = 0; i < PT::m(); ++i) t[i] = am.rR[i] * (ahr[i] - (bR[i] - axp[i]));
         }
         chol_solve_inv<PT>(K.M, t);   // inactive rows: identity, t stays 0
         double atdz[NN];
@@ -916,26 +979,54 @@ PHX_LD void kkt_refine(const Data<PT>& D, const ASet<PT>& a, const KFactor<PT>& 
         // refinement is not monotone, and the cut rounds moved the active set
         // to another optimal vertex.)
         const double tol2 = KKT_STOP * KKT_STOP * (1.0 + x2);
+        PHX_REFINE_HOOK(it, d2, tol2);
         if (d2 <= tol2) break;
+#ifdef PHX_REFINE_PREDICT
+        // (opt-in, measured and not adopted, r04) The refinement contracts
+        // geometrically (emulation, farmer: relative corrections 1e-0.3,
+        // 1e-4.1, 1e-7.8, 1e-11.6 over a 4-step solve); stopping once the
+        // PREDICTED next correction, (d / d_prev) d, passes the stop saves the
+        // confirming step (3.67 -> 2.7 steps per round) but leaves errors at the
+        // stop's scale instead of 1e-4 below it: 6e-10 in aircond's W, and
+        // x-bar points whose rows are violated by ~1e-9 relative, which a
+        // fixed-nonant evaluation of x-bar (the x-bar inner bound) rejects.
+        if (d2 <= 1e-12 * (1.0 + x2) && d2 <= 1e-4 * dprev2 && d2 * d2 <= tol2 * dprev2) break;
+        dprev2 = d2;
+#endif
     }
 }
 
 // right-hand sides: the lane's own problem; the affine parts of the map
+// (xb: the value of a non-free column; b: the active side of a row -- both
+// always finite, chosen by the finiteness structure where it decides: a
+// non-free column sits at a finite bound and an active row at a finite side,
+// so only where both are finite does the active set's bit select; the value
+// for a free column / inactive row is never used, only multiplied by 0)
+template <class PT>
+PHX_LD double bound_of(const Data<PT>& D, const ASet<PT>& a, int j) {
+    if (PT::lfin(j) && PT::ufin(j)) return a.up(j) ? D.u(j) : D.l(j);
+    return PT::ufin(j) ? D.u(j) : (PT::lfin(j) ? D.l(j) : 0.0);
+}
+template <class PT>
+PHX_LD double side_of(const Data<PT>& D, const ASet<PT>& a, int i) {
+    if (PT::blfin(i) && PT::bufin(i)) return a.lo(i) ? D.bl(i) : D.bu(i);
+    return PT::blfin(i) ? D.bl(i) : (PT::bufin(i) ? D.bu(i) : 0.0);
+}
 template <class PT>
 struct RhsFull {
     const Data<PT>& D;
     const ASet<PT>& a;
     PHX_LD double q(int j) const { return D.q(j); }
-    PHX_LD double xb(int j) const { return a.up(j) ? D.u(j) : D.l(j); }
-    PHX_LD double b(int i) const { return a.lo(i) ? D.bl(i) : D.bu(i); }
+    PHX_LD double xb(int j) const { return bound_of<PT>(D, a, j); }
+    PHX_LD double b(int i) const { return side_of<PT>(D, a, i); }
 };
 template <class PT>
 struct RhsBase {      // the PH terms off: q = c
     const Data<PT>& D;
     const ASet<PT>& a;
     PHX_LD double q(int j) const { return D.c(j); }
-    PHX_LD double xb(int j) const { return a.up(j) ? D.u(j) : D.l(j); }
-    PHX_LD double b(int i) const { return a.lo(i) ? D.bl(i) : D.bu(i); }
+    PHX_LD double xb(int j) const { return bound_of<PT>(D, a, j); }
+    PHX_LD double b(int i) const { return side_of<PT>(D, a, i); }
 };
 template <class PT>
 struct RhsSlot {      // d/dqn[t]: unit linear term on slot t's column, homogeneous otherwise
@@ -955,8 +1046,9 @@ struct RhsSlot {      // d/dqn[t]: unit linear term on slot t's column, homogene
 template <class PT>
 PHX_LD bool kkt_solve(const Data<PT>& D, const ASet<PT>& a, double* xp, double* z) {
     KFactor<PT> K;
-    if (!kkt_factor<PT>(D, a, K)) return false;
-    kkt_refine<PT>(D, a, K, RhsFull<PT>{D, a}, xp, z);
+    const AMul<PT> am(a);
+    if (!kkt_factor<PT>(D, am, K)) return false;
+    kkt_refine<PT>(D, am, K, RhsFull<PT>{D, a}, xp, z);
     return true;
 }
 
@@ -979,13 +1071,14 @@ PHX_LD bool map_compute(const Data<PT>& D, const ASet<PT>& a, const LaneIO& io, 
     const int64_t S = io.S;
     const int W = PT::n() + PT::m();
     KFactor<PT> K;
-    if (!kkt_factor<PT>(D, a, K)) return false;
+    const AMul<PT> am(a);
+    if (!kkt_factor<PT>(D, am, K)) return false;
     PHX_NOUNROLL for (int t = -1; t < PT::nslot(); ++t) {
         double xp[NN], z[MM];
         PHX_UNROLL for (int j = 0; j < PT::n(); ++j) xp[j] = 0.0;
         PHX_UNROLL for (int i = 0; i < PT::m(); ++i) z[i] = 0.0;
-        if (t < 0) kkt_refine<PT>(D, a, K, RhsBase<PT>{D, a}, xp, z);
-        else kkt_refine<PT>(D, a, K, RhsSlot<PT>{D, t}, xp, z);
+        if (t < 0) kkt_refine<PT>(D, am, K, RhsBase<PT>{D, a}, xp, z);
+        else kkt_refine<PT>(D, am, K, RhsSlot<PT>{D, t}, xp, z);
         double* m = io.map + (int64_t)(t + 1) * W * S + sc;
         PHX_UNROLL for (int j = 0; j < PT::n(); ++j) m[(int64_t)j * S] = xp[j];
         PHX_UNROLL for (int i = 0; i < PT::m(); ++i) m[(int64_t)(PT::n() + i) * S] = z[i];
@@ -1031,7 +1124,7 @@ PHX_LD int worst_violation(const Data<PT>& D, CM enter_lo, CM enter_up, CM leave
     D.matvec(xp, axp);
     PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
         const double d = D.dc(j);
-        const double lam = (D.q(j) + D.p(j) * xp[j] + atz[j]) * D.idc(j);
+        const double lam = (D.qpx(j, xp[j]) + atz[j]) * D.idc(j);
         if (PT::lfin(j)) {
             const double v = (D.l(j) - xp[j]) * d * rcp_step(1.0 + fabs(D.l(j) * d));
             const bool f = ((enter_lo >> j) & 1) && v > bp;
@@ -1087,8 +1180,10 @@ PHX_LD int certify_update(const Data<PT>& D, ASet<PT>& a, const double* xp, cons
     PHX_UNROLL for (int j = 0; j < PT::n(); ++j) qmax = fmax(qmax, fabs(D.q(j) * D.idc(j)));
     const double dtol = kkt_tol * (1.0 + qmax);
     const double ptol = kkt_tol;
-    // branch-free: violations are gathered into bit masks, applied at the end
-    bool bad = false;                 // a violation the active set cannot fix
+    // branch-free: violations are gathered into bit masks, applied at the end;
+    // each condition is a 0/1 integer in a vector register (vbit), never a
+    // live lane mask
+    uint32_t bad = 0;                 // a violation the active set cannot fix
     CM enter_lo = 0, enter_up = 0, leave = 0;
     double atz[PT::NMAX_N];
     D.matvec_t(z, atz);
@@ -1099,20 +1194,20 @@ PHX_LD int certify_update(const Data<PT>& D, ASet<PT>& a, const double* xp, cons
     double fin = 0.0;
     PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
         const double d = D.dc(j);
-        const double lam = (D.q(j) + D.p(j) * xp[j] + atz[j]) * D.idc(j);
+        const double lam = (D.qpx(j, xp[j]) + atz[j]) * D.idc(j);
         fin = fma(lam, 0.0, fin);
-        const bool F = a.F(j), U = a.up(j);
-        bool below = false, above = false;
+        const uint32_t F = (uint32_t)(a.f >> j) & 1u, U = (uint32_t)(a.u >> j) & 1u;
+        uint32_t below = 0, above = 0;
         if (PT::lfin(j)) {
             const double lo = D.l(j);
-            below = F && xp[j] < lo && (lo - xp[j]) * d > ptol * (1.0 + fabs(lo * d));
+            below = F & vbit(xp[j] < lo && (lo - xp[j]) * d > ptol * (1.0 + fabs(lo * d)));
         }
         if (PT::ufin(j)) {
             const double hi = D.u(j);
-            above = F && !below && xp[j] > hi && (xp[j] - hi) * d > ptol * (1.0 + fabs(hi * d));
+            above = F & (below ^ 1u) & vbit(xp[j] > hi && (xp[j] - hi) * d > ptol * (1.0 + fabs(hi * d)));
         }
-        bad = bad || (F && !below && !above && fabs(lam) > dtol);
-        const bool lv = !PT::fixed(j) && !F && (U ? lam > dtol : lam < -dtol);
+        bad |= F & ((below | above) ^ 1u) & vbit(fabs(lam) > dtol);
+        const uint32_t lv = PT::fixed(j) ? 0u : (F ^ 1u) & ((U & vbit(lam > dtol)) | ((U ^ 1u) & vbit(lam < -dtol)));
         enter_lo |= (CM)below << j;
         enter_up |= (CM)above << j;
         leave |= (CM)lv << j;
@@ -1123,22 +1218,22 @@ PHX_LD int certify_update(const Data<PT>& D, ASet<PT>& a, const double* xp, cons
     PHX_UNROLL for (int i = 0; i < PT::m(); ++i) {
         const double d = D.dr(i), id = D.idr(i);
         fin = fma(axp[i], 0.0, fma(z[i], 0.0, fin));
-        const bool R = a.R(i), L = a.lo(i);
-        bool below = false, above = false;
+        const uint32_t R = (a.r >> i) & 1u, L = (a.l >> i) & 1u;
+        uint32_t below = 0, above = 0;
         if (PT::blfin(i)) {
             const double lo = D.bl(i);
-            below = axp[i] < lo && (lo - axp[i]) * id > ptol * (1.0 + fabs(lo * id));
+            below = vbit(axp[i] < lo && (lo - axp[i]) * id > ptol * (1.0 + fabs(lo * id)));
         }
         if (PT::bufin(i)) {
             const double hi = D.bu(i);
-            above = axp[i] > hi && (axp[i] - hi) * id > ptol * (1.0 + fabs(hi * id));
+            above = vbit(axp[i] > hi && (axp[i] - hi) * id > ptol * (1.0 + fabs(hi * id)));
         }
-        bad = bad || (R && (below || above));
+        bad |= R & (below | above);
         const double yy = -z[i] * d;
-        const bool dr = !PT::eq(i) && R && (L ? yy < -dtol : yy > dtol);
-        act_lo |= (uint32_t)(!R && below) << i;
-        act_up |= (uint32_t)(!R && !below && above) << i;
-        drop |= (uint32_t)dr << i;
+        const uint32_t dr = PT::eq(i) ? 0u : R & ((L & vbit(yy < -dtol)) | ((L ^ 1u) & vbit(yy > dtol)));
+        act_lo |= ((R ^ 1u) & below) << i;
+        act_up |= ((R ^ 1u) & (below ^ 1u) & above) << i;
+        drop |= dr << i;
     }
     if (!(fin == 0.0)) return 2;      // not certified, and no update can repair it
     const bool changed = (enter_lo | enter_up | leave) != 0 || (act_lo | act_up | drop) != 0;
@@ -1160,7 +1255,7 @@ PHX_LD int certify_update(const Data<PT>& D, ASet<PT>& a, const double* xp, cons
     a.u = (a.u & ~(enter_lo | leave)) | enter_up;
     a.r = (a.r | act_lo | act_up) & ~drop;
     a.l = (a.l & ~act_up) | act_lo;
-    return changed ? 1 : (bad ? 2 : 0);
+    return changed ? 1 : (bad != 0 ? 2 : 0);
 }
 
 // KKT solve / certificate / active-set update rounds from (a, xp, z): full
@@ -1562,19 +1657,28 @@ __device__ bool fz_prologue(const LaneIO& io) {
 
 // Update_W for one lane (in place, before its Data reads W): returns the
 // lane's sum |x_{k-1} - x-bar_k| over its nonant slots.
+// (fused mode: one tree node, node slot = nonant slot -- x-bar of slot t is
+// stage[t], no index gather; all loads issued before the stores)
 template <class PT>
 __device__ double fz_update_w(const LaneIO& io, int sc) {
     const FusedW& f = io.fz;
     const int64_t S = io.S;
-    double d = 0.0;
+    constexpr int NS = PT::nslot() > 0 ? PT::nslot() : 1;
+    double xv[NS], wv[NS], rv[NS];
     PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
         const int t = PT::col_slot(j);
         if (t >= 0) {
             const int64_t o = (int64_t)t * S + sc;
-            const double diff = f.x_prev[(int64_t)j * S + sc] - f.stage[io.xbar_idx[o]];
-            PHX_OUT(const_cast<double*>(io.W)[o], io.W[o] + io.rho[o] * diff);
-            d += fabs(diff);
+            xv[t] = f.x_prev[(int64_t)j * S + sc];
+            wv[t] = io.W[o];
+            rv[t] = io.rho[o];
         }
+    }
+    double d = 0.0;
+    PHX_UNROLL for (int t = 0; t < PT::nslot(); ++t) {
+        const double diff = xv[t] - f.stage[t];
+        PHX_OUT(const_cast<double*>(io.W)[(int64_t)t * S + sc], wv[t] + rv[t] * diff);
+        d += fabs(diff);
     }
     return d;
 }
@@ -1597,14 +1701,14 @@ __device__ void fz_epilogue(const LaneIO& io, int sc, bool still) {
     double v[NV];
     PHX_UNROLL for (int e = 0; e < NV; ++e) v[e] = 0.0;
     if (sc < io.S) {
-        double dl = 0.0;
+        // (the same slot order and operations as fz_update_w)
+        double xv[NS];
         PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
             const int t = PT::col_slot(j);
-            if (t >= 0) {
-                const int64_t o = (int64_t)t * S + sc;
-                dl += fabs(f.x_prev[(int64_t)j * S + sc] - f.stage[io.xbar_idx[o]]);
-            }
+            if (t >= 0) xv[t] = f.x_prev[(int64_t)j * S + sc];
         }
+        double dl = 0.0;
+        PHX_UNROLL for (int t = 0; t < PT::nslot(); ++t) dl += fabs(xv[t] - f.stage[t]);
         v[2 * NS] = dl;
         if (!still)
             PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
