@@ -938,35 +938,42 @@ PHX_LD void kkt_refine(const Data<PT>& D, const AMul<PT>& am, const KFactor<PT>&
 #ifdef PHX_REFINE_PREDICT
     double dprev2 = 1e300;
 #endif
+    // A'z is carried from step to step (z += t  =>  A'z += A't: 12 adds instead
+    // of a mat-vec), and x2, the stop's scale, is the first step's (the step
+    // that moves the point; the later ones change it by the refinement's
+    // corrections only)
+    double atz[NN];
+    D.matvec_t(z, atz);
+    double x2 = 0.0;
     PHX_REFINE_LOOP for (int it = 0; it < KKT_REFINE; ++it) {
         double g[NN], t[MM];
+        PHX_UNROLL for (int j = 0; j < PT::n(); ++j)
+            g[j] = (PT::col_slot(j) >= 0 ? -R.q(j) - D.p(j) * xp[j] : -R.q(j)) - atz[j];
         {
-            double atz[NN];
-            D.matvec_t(z, atz);
-            PHX_UNROLL for (int j = 0; j < PT::n(); ++j)
-                g[j] = (PT::col_slot(j) >= 0 ? -R.q(j) - D.p(j) * xp[j] : -R.q(j)) - atz[j];
-        }
-        {
-            double axp[MM], hr[NN], ahr[MM];
-            D.matvec(xp, axp);
-            PHX_UNROLL for (int j = 0; j < PT::n(); ++j) hr[j] = g[j] * hf[j];
-            D.matvec(hr, ahr);
-            PHX_UNROLL for (int i = 0; i < PT::m(); ++i) t[i] = am.rR[i] * (ahr[i] - (bR[i] - axp[i]));
+            // t = A_R (xp + H_F g) - b_R: one mat-vec of the sum (the same
+            // rounding as the two products it replaces, to eps |A| |x|)
+            double u[NN], au[MM];
+            PHX_UNROLL for (int j = 0; j < PT::n(); ++j) u[j] = fma(g[j], hf[j], xp[j]);
+            D.matvec(u, au);
+            PHX_UNROLL for (int i = 0; i < PT::m(); ++i) t[i] = am.rR[i] * (au[i] - bR[i]);
         }
         chol_solve_inv<PT>(K.M, t);   // inactive rows: identity, t stays 0
         double atdz[NN];
         D.matvec_t(t, atdz);
-        double d2 = 0.0, x2 = 0.0;
+        double d2 = 0.0;
         PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
             const double d = (g[j] - atdz[j]) * hf[j];
             xp[j] += d;
             d2 += d * d;
-            x2 += xp[j] * xp[j];
+            atz[j] += atdz[j];
         }
         PHX_UNROLL for (int i = 0; i < PT::m(); ++i) {
             z[i] += t[i];
             d2 += t[i] * t[i];
-            x2 += z[i] * z[i];
+        }
+        if (it == 0) {
+            PHX_UNROLL for (int j = 0; j < PT::n(); ++j) x2 += xp[j] * xp[j];
+            PHX_UNROLL for (int i = 0; i < PT::m(); ++i) x2 += z[i] * z[i];
         }
         PHX_LANE_STAT(1);
         // stop once the correction vanishes (1e-10 relative, in squared 2-norms:

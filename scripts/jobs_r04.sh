@@ -15,5 +15,8 @@ case "$1" in
        PHX_LANE_STAMPS=1 $J "bench:r04_s1_c3s8_stamps:$S8" ;;
   s2)  $J "test:tests" "bench:r04_s2_c3s8:$S8" "bench:r04_s2_bench:$H" "prof:r04_s2_c3s8_prof:$S8" && \
        PHX_LANE_DEFS=PHX_RELAXED_HANDOFF $J "bench:r04_s2_bench_relaxed:$H" "bench:r04_s2_c3s8_relaxed:$S8" ;;
+  s3)  $J "test:tests/test_gpu_parity.py tests/test_trajectories.py tests/test_hydro.py" "bench:r04_s3_c3s8:$S8" \
+          "bench:r04_s3_bench:$H" "prof:r04_s3_prof:$H --ar-probe 0" "prof:r04_s3_c3s8_prof:$S8" && \
+       PHX_LANE_STAMPS=1 $J "bench:r04_s3_c3s8_stamps:$S8" "bench:r04_s3_stamps:$H --ar-probe 0" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
