@@ -1613,6 +1613,28 @@ __device__ bool arrive_last(unsigned int* tk, unsigned int nblocks) {
     return s_last != 0u;
 }
 
+// Sum over a full wavefront (all 64 lanes active), uniform result: DPP
+// moves within rows of 16 lanes (quad perms, half-row and row mirrors), then
+// the row broadcasts of lanes 15 and 31 -- VALU-only steps, where __shfl_down
+// was a chain of six ds_bpermute round trips through the LDS crossbar per
+// value.  A fixed order: bitwise reproducible.
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ double dpp_add(double v) {
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u & 0xffffffffull), CTRL, ROWMASK, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, ROWMASK, 0xf, false);
+    return v + __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+__device__ __forceinline__ double wave_sum(double v) {
+    v = dpp_add<0xB1, 0xf>(v);     // quad_perm [1,0,3,2]
+    v = dpp_add<0x4E, 0xf>(v);     // quad_perm [2,3,0,1]
+    v = dpp_add<0x141, 0xf>(v);    // row_half_mirror
+    v = dpp_add<0x140, 0xf>(v);    // row_mirror: every lane of a row holds its sum
+    v = dpp_add<0x142, 0xa>(v);    // row_bcast:15 into rows 1, 3
+    v = dpp_add<0x143, 0xc>(v);    // row_bcast:31 into rows 2, 3: lane 63 holds the total
+    return __longlong_as_double(__builtin_amdgcn_readlane(__double_as_longlong(v), 63));
+}
+
 __device__ __forceinline__ void publish_progress(IterkProgress* p, int iter, int done, double conv) {
     // relaxed system-scope stores: no fence (a system release would write back
     // and invalidate the L2); the host orders nothing else on this word
@@ -1728,8 +1750,7 @@ __device__ void fz_epilogue(const LaneIO& io, int sc, bool still) {
                 }
             }
     }
-    PHX_UNROLL for (int e = 0; e < NV; ++e)
-        for (int off = 32; off > 0; off >>= 1) v[e] += __shfl_down(v[e], off, 64);
+    PHX_UNROLL for (int e = 0; e < NV; ++e) v[e] = wave_sum(v[e]);
     const unsigned nb = gridDim.x, b = blockIdx.x, k = b % TICKET_SHARDS;
     const unsigned nk = (nb - k + TICKET_SHARDS - 1) / TICKET_SHARDS;
     const unsigned nsh = nb < TICKET_SHARDS ? nb : TICKET_SHARDS;
@@ -1756,8 +1777,7 @@ __device__ void fz_epilogue(const LaneIO& io, int sc, bool still) {
         }
         PHX_UNROLL for (int u = 0; u < 4; ++u) PHX_UNROLL for (int e = 0; e < NV; ++e) v[e] += l[u][e];
     }
-    PHX_UNROLL for (int e = 0; e < NV; ++e)
-        for (int off = 32; off > 0; off >>= 1) v[e] += __shfl_down(v[e], off, 64);
+    PHX_UNROLL for (int e = 0; e < NV; ++e) v[e] = wave_sum(v[e]);
     __syncthreads();
     if (threadIdx.x == 0) {
         PHX_UNROLL for (int e = 0; e < NV; ++e) store_wt(&shard_part[k * NV + e], v[e]);
