@@ -243,6 +243,17 @@ inline std::string lane_kernel_source(const LaneStructure& L, int warm_waves = 1
          "  if (io.fz.on) phx_lane::fz_epilogue<PT>(io, t, still);\n"
          "  phx_lane::lane_stamp(io, 5);\n"
          "}\n";
+    // phx_iterk fused mode: one whole PH iteration per launch, every load of
+    // the lane's Update_W and first round issued at entry (phx_lane.h warm_fused)
+    o << "extern \"C\" __global__ void __launch_bounds__(64, " << warm_waves
+      << ") phx_lane_warm_fz(phx_lane::LaneIO io) {\n"
+         "  phx_lane::warm_fused<PT>(io);\n"
+         "}\n";
+    // ... for batches of at most one wavefront per SIMD: the whole register
+    // file (VGPRs + AGPRs) for one wave, no scratch spills
+    o << "extern \"C\" __global__ void __launch_bounds__(64, 1) phx_lane_warm_fz1(phx_lane::LaneIO io) {\n"
+         "  phx_lane::warm_fused<PT>(io);\n"
+         "}\n";
     // phx_iterk fused mode, after the last enqueued iteration: the decision on
     // its conv (the next warm launch's prologue does it otherwise)
     o << "extern \"C\" __global__ void __launch_bounds__(64) phx_fz_tail(phx_lane::LaneIO io) {\n"

@@ -260,6 +260,23 @@ struct Data {
             kn += 0.5 * r * xb * xb;
         }
     }
+    // From values already in registers (the fused kernel's preloads, phx_lane_warm_fz):
+    // the varying A values, W and rho of every slot and x-bar by slot -- the
+    // same operations as the loading constructor, so the same bits
+    PHX_LD Data(const LaneIO& io_, int sc_, const double* av_, const double* wv, const double* rv, const double* xbv)
+        : io(io_), sc(sc_) {
+        PHX_UNROLL for (int v = 0; v < PT::nvar(); ++v) av[v] = av_[v];
+        const bool won = io.W_on != 0, pon = io.prox_on != 0;
+        kn = 0.0;
+        PHX_UNROLL for (int t = 0; t < PT::nslot(); ++t) {
+            const double xb = xbv[t];
+            const double r = pon ? rv[t] : 0.0;
+            const double w = won ? wv[t] : 0.0;
+            qn[t] = w - r * xb;
+            pn[t] = r;
+            kn += 0.5 * r * xb * xb;
+        }
+    }
     PHX_LD double A(int k) const { return PT::kvar(k) < 0 ? PT::Ac(k) : av[PT::kvar(k)]; }
     // scaling of the problem the lane solver works on (1 when unscaled)
     PHX_LD double dc(int j) const { return PT::scaled() ? PT::dcs(j) : 1.0; }
@@ -797,10 +814,17 @@ struct AMul {
 };
 
 template <class PT>
+PHX_LD void aset_from_words(const uint32_t* w, ASet<PT>& a);
+template <class PT>
 PHX_LD void aset_load(const LaneIO& io, int sc, ASet<PT>& a) {
     constexpr int NW = aset_words(PT::NMAX_N, PT::NMAX_M);
     uint32_t w[NW];
     PHX_UNROLL for (int k = 0; k < aset_words(PT::n(), PT::m()); ++k) w[k] = io.aset[(int64_t)k * io.S + sc];
+    aset_from_words<PT>(w, a);
+}
+// the active set from its stored words (2 bits per column, then per row)
+template <class PT>
+PHX_LD void aset_from_words(const uint32_t* w, ASet<PT>& a) {
     PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
         const uint32_t v = (w[(2 * j) >> 5] >> ((2 * j) & 31)) & 3u;
         bool fr = !PT::fixed(j) && v == 0u;
@@ -938,17 +962,20 @@ PHX_LD void kkt_refine(const Data<PT>& D, const AMul<PT>& am, const KFactor<PT>&
 #ifdef PHX_REFINE_PREDICT
     double dprev2 = 1e300;
 #endif
-    // A'z is carried from step to step (z += t  =>  A'z += A't: 12 adds instead
-    // of a mat-vec), and x2, the stop's scale, is the first step's (the step
-    // that moves the point; the later ones change it by the refinement's
-    // corrections only)
-    double atz[NN];
-    D.matvec_t(z, atz);
+    // x2, the stop's scale, is the first step's (the step that moves the
+    // point; the later ones change it by the refinement's corrections only).
+    // (Carrying A'z from step to step -- A'z += A't, 12 adds instead of a
+    // mat-vec -- kept 12 more values live across the loop: 12 -> 72 B of
+    // scratch per lane in the warm kernel, r04.)
     double x2 = 0.0;
     PHX_REFINE_LOOP for (int it = 0; it < KKT_REFINE; ++it) {
         double g[NN], t[MM];
-        PHX_UNROLL for (int j = 0; j < PT::n(); ++j)
-            g[j] = (PT::col_slot(j) >= 0 ? -R.q(j) - D.p(j) * xp[j] : -R.q(j)) - atz[j];
+        {
+            double atz[NN];
+            D.matvec_t(z, atz);
+            PHX_UNROLL for (int j = 0; j < PT::n(); ++j)
+                g[j] = (PT::col_slot(j) >= 0 ? -R.q(j) - D.p(j) * xp[j] : -R.q(j)) - atz[j];
+        }
         {
             // t = A_R (xp + H_F g) - b_R: one mat-vec of the sum (the same
             // rounding as the two products it replaces, to eps |A| |x|)
@@ -965,7 +992,6 @@ PHX_LD void kkt_refine(const Data<PT>& D, const AMul<PT>& am, const KFactor<PT>&
             const double d = (g[j] - atdz[j]) * hf[j];
             xp[j] += d;
             d2 += d * d;
-            atz[j] += atdz[j];
         }
         PHX_UNROLL for (int i = 0; i < PT::m(); ++i) {
             z[i] += t[i];
@@ -1273,13 +1299,32 @@ PHX_LD int certify_update(const Data<PT>& D, ASet<PT>& a, const double* xp, cons
 // and the round's pair products / reciprocals hoisted with it stayed live
 // across the loop, spilled ~200 B of scratch per lane and doubled the warm
 // kernel's memory traffic; re-read, it comes from L2.
+// D0: the first round's data when the caller has it in registers already
+// (the fused kernel); write_its >= 0: a certified lane's outputs are written
+// here from the certifying round's data (write_certified, no reload), and with
+// pc its x-bar partials [sum pc x | sum pc x^2 per slot] are added to part.
 template <class PT>
-PHX_LD bool as_rounds(const LaneIO& io, int sc, ASet<PT>& a, int rounds, double* xp, double* z) {
-    PHX_NOUNROLL for (int r = 0; r < rounds; ++r) {
-        PHX_LANE_STAT(0);
+PHX_LD void write_certified(const LaneIO& io, const Data<PT>& D, int sc, const ASet<PT>& a, const double* xp,
+                            const double* z, int its, bool map_ok = false);
+// One round with the given data: KKT solve, certificate, active-set update
+// (0 certified, 1 active set changed, 2 not certified and nothing to change,
+// 3 the Schur complement was not positive definite).
+template <class PT>
+PHX_LD int as_round(const LaneIO& io, const Data<PT>& D, ASet<PT>& a, double* xp, double* z, int r) {
+    PHX_LANE_STAT(0);
+    if (!kkt_solve<PT>(D, a, xp, z)) return 3;
+    return certify_update<PT>(D, a, xp, z, io.kkt_tol, r >= io.single_after);
+}
+// r0: the index of the first round (the fused kernel runs round 0 itself)
+// (a certified lane is written by the caller from re-loaded data: writing it
+// inside the loop kept the round's data live through the outputs and spilled
+// ~400 B per lane, r04)
+template <class PT>
+PHX_LD bool as_rounds(const LaneIO& io, int sc, ASet<PT>& a, int rounds, double* xp, double* z, int r0 = 0) {
+    PHX_NOUNROLL for (int r = r0; r < rounds; ++r) {
         const Data<PT> D(io, opaque_index(sc));
-        if (!kkt_solve<PT>(D, a, xp, z)) return false;
-        const int c = certify_update<PT>(D, a, xp, z, io.kkt_tol, r >= io.single_after);
+        const int c = as_round<PT>(io, D, a, xp, z, r);
+        if (c == 3) return false;
         if (c == 0) return true;
         if (c == 2) { PHX_LANE_STAT(3); return false; }
     }
@@ -1380,7 +1425,7 @@ PHX_LD void seed_fill(const LaneIO& io, int sc, const int32_t* tl, int T, const 
 // Certified lane: unscaled outputs, objective (incl. PH terms), active set.
 template <class PT>
 PHX_LD void write_certified(const LaneIO& io, const Data<PT>& D, int sc, const ASet<PT>& a, const double* xp,
-                            const double* z, int its, bool map_ok = false) {
+                            const double* z, int its, bool map_ok) {
     const int S = io.S;
     double f = D.kn;
     PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
@@ -1722,6 +1767,8 @@ __device__ double fz_update_w(const LaneIO& io, int sc) {
 // operations in the same order as fz_update_w: carried across the solve it was
 // one of the values spilled to scratch)
 template <class PT>
+__device__ void fz_fold(const LaneIO& io, double* v);
+template <class PT>
 __device__ void fz_epilogue(const LaneIO& io, int sc, bool still) {
     const FusedW& f = io.fz;
     constexpr int NS = PT::nslot() > 0 ? PT::nslot() : 1;
@@ -1750,6 +1797,16 @@ __device__ void fz_epilogue(const LaneIO& io, int sc, bool still) {
                 }
             }
     }
+    fz_fold<PT>(io, v);
+}
+
+// The fold of the lanes' partials v[2 NS + 1] (the wavefront's sums, then the
+// blocks' and the shards' in fixed orders).  Every lane of the block calls it.
+template <class PT>
+__device__ void fz_fold(const LaneIO& io, double* v) {
+    const FusedW& f = io.fz;
+    constexpr int NS = PT::nslot() > 0 ? PT::nslot() : 1;
+    constexpr int NV = 2 * NS + 1;
     PHX_UNROLL for (int e = 0; e < NV; ++e) v[e] = wave_sum(v[e]);
     const unsigned nb = gridDim.x, b = blockIdx.x, k = b % TICKET_SHARDS;
     const unsigned nk = (nb - k + TICKET_SHARDS - 1) / TICKET_SHARDS;
@@ -1878,6 +1935,105 @@ __device__ __forceinline__ void compact_lane(bool still, int sc, int32_t* out, i
     base = __shfl(base, 0, 64);
     if (still) out[base + __popcll(b & ((1ull << lane) - 1ull))] = sc;
 }
+// A whole fused PH iteration (phx_iterk fused mode, kernel phx_lane_warm_fz).
+// Every load of the lane's Update_W and of its first active-set round is
+// issued at kernel entry, before the gate and the stop decision are known
+// (loads have no effects; a gated launch just drops them): the lane's varying
+// A values, its active-set words, and per slot x_{k-1}, W, rho and prob_coeff.
+// Update_W then runs in registers and hands the new W straight to the first
+// round's data (no re-load of what it just stored); a certified lane's
+// outputs and x-bar partials come from the certifying round's registers
+// (as_rounds), so the epilogue re-reads nothing.  The same operations as
+// phx_lane_warm's fused path (fz_update_w, warm_lane, fz_epilogue).
+template <class PT>
+__device__ void warm_fused(const LaneIO& io) {
+    const FusedW& f = io.fz;
+    constexpr int NS = PT::nslot() > 0 ? PT::nslot() : 1;
+    constexpr int NV = 2 * NS + 1;
+    constexpr int NVA = PT::NMAX_V, NW = aset_words(PT::NMAX_N, PT::NMAX_M);
+    const int sc = blockIdx.x * 64 + threadIdx.x;
+    const bool live = sc < io.S;
+    const int s = live ? sc : 0;            // (tail lanes load lane 0's values: valid addresses, unused)
+    const int64_t S = io.S;
+    double av[NVA], xv[NS], wv[NS], rv[NS], pcv[NS];
+    uint32_t aw[NW];
+    PHX_UNROLL for (int v = 0; v < PT::nvar(); ++v) av[v] = io.Av[(int64_t)v * S + s];
+    PHX_UNROLL for (int k = 0; k < aset_words(PT::n(), PT::m()); ++k) aw[k] = io.aset[(int64_t)k * S + s];
+    PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
+        const int t = PT::col_slot(j);
+        if (t >= 0) {
+            const int64_t o = (int64_t)t * S + s;
+            xv[t] = f.x_prev[(int64_t)j * S + s];
+            wv[t] = io.W[o];
+            rv[t] = io.rho[o];
+            pcv[t] = f.pc[o];
+        }
+    }
+    lane_stamp(io, 0);
+    if (gated(io.gate)) return;
+    if (!fz_prologue(io)) return;
+    zero_next_counts(io.counts_next);
+    lane_stamp(io, 1);
+    // Update_W (phbase.py:293-318) and |x_{k-1} - x-bar_k| (convergence_diff)
+    double xb[NS], dl = 0.0;
+    PHX_UNROLL for (int t = 0; t < PT::nslot(); ++t) {
+        xb[t] = f.stage[t];
+        const double diff = xv[t] - xb[t];
+        wv[t] = wv[t] + rv[t] * diff;
+        if (live) PHX_OUT(const_cast<double*>(io.W)[(int64_t)t * S + sc], wv[t]);
+        dl += fabs(diff);
+    }
+    lane_stamp(io, 2);
+    bool still = false;
+    double xn[NS];                      // the certified lane's unscaled nonant x
+    if (live) {
+        ASet<PT> a;
+        aset_from_words<PT>(aw, a);
+        double xp[PT::NMAX_N], z[PT::NMAX_M];
+        PHX_UNROLL for (int j = 0; j < PT::n(); ++j) xp[j] = 0.0;
+        PHX_UNROLL for (int i = 0; i < PT::m(); ++i) z[i] = 0.0;
+        // round 0 on the data in registers; later rounds re-load (as_rounds)
+        int c;
+        {
+            const Data<PT> D0(io, sc, av, wv, rv, xb);
+            c = io.warm_rounds > 0 ? as_round<PT>(io, D0, a, xp, z, 0) : 2;
+            if (c == 0) write_certified<PT>(io, D0, sc, a, xp, z, 0);
+        }
+        if (c == 1 && as_rounds<PT>(io, sc, a, io.warm_rounds, xp, z, 1)) {
+            c = 0;
+            const Data<PT> Dc(io, opaque_index(sc));
+            write_certified<PT>(io, Dc, sc, a, xp, z, 0);
+        }
+        if (c != 0) {
+            aset_store<PT>(io, sc, a);   // the updated active set seeds the next pass
+            io.status[sc] = 0;
+            io.flags[sc] = 0;
+            still = true;
+        } else {
+            PHX_UNROLL for (int j = 0; j < PT::n(); ++j)
+                if (PT::col_slot(j) >= 0) xn[PT::col_slot(j)] = xp[j] * (PT::scaled() ? PT::dcs(j) : 1.0);
+        }
+    }
+    // the lane's x-bar partials (a certified lane's unscaled x as written) and
+    // its convergence term
+    double v[NV];
+    PHX_UNROLL for (int e = 0; e < NV; ++e) v[e] = 0.0;
+    if (live) {
+        v[2 * NS] = dl;
+        if (!still)
+            PHX_UNROLL for (int t = 0; t < PT::nslot(); ++t) {
+                const double w = pcv[t] * xn[t];
+                v[t] += w;
+                v[NS + t] += w * xn[t];
+            }
+    }
+    lane_stamp(io, 3);
+    compact_lane(still, sc, io.lanes_out, io.count_out);
+    lane_stamp(io, 4);
+    fz_fold<PT>(io, v);
+    lane_stamp(io, 5);
+}
+
 #endif
 
 }  // namespace phx_lane
