@@ -1677,7 +1677,11 @@ __device__ __forceinline__ double wave_sum(double v) {
     v = dpp_add<0x140, 0xf>(v);    // row_mirror: every lane of a row holds its sum
     v = dpp_add<0x142, 0xa>(v);    // row_bcast:15 into rows 1, 3
     v = dpp_add<0x143, 0xc>(v);    // row_bcast:31 into rows 2, 3: lane 63 holds the total
-    return __longlong_as_double(__builtin_amdgcn_readlane(__double_as_longlong(v), 63));
+    // (readlane is 32-bit: a 64-bit argument would be truncated to its low half)
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u & 0xffffffffull), 63);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), 63);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
 __device__ __forceinline__ void publish_progress(IterkProgress* p, int iter, int done, double conv) {

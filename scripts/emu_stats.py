@@ -32,6 +32,7 @@ lib = _native.Lib(%(so)r, prefix="emu_phx_")
 S, K = %(S)d, %(K)d
 opts = ph_options(K)
 opts["iterk_solver_options"] = {"native_loop": 0}
+opts["iter0_solver_options"] = dict(%(so0)s)
 ph = PH(opts, farmer.scenario_names_creator(S), farmer.scenario_creator, scenario_creator_kwargs={"num_scens": S},
         _native_lib=lib, _device="cpu")
 conv, E, tb = ph.ph_main()
@@ -47,7 +48,8 @@ def main():
     K = int(pos[1]) if len(pos) > 1 else 10
     so = build(flags)
     env = dict(os.environ, PHX_EMU_DEBUG="1")
-    r = subprocess.run([sys.executable, "-c", CHILD % {"root": _ROOT, "so": so, "S": S, "K": K}],
+    so0 = os.environ.get("EMU_SO0", "{}")
+    r = subprocess.run([sys.executable, "-c", CHILD % {"root": _ROOT, "so": so, "S": S, "K": K, "so0": so0}],
                        capture_output=True, text=True, env=env)
     k = 0
     for line in r.stderr.splitlines():
@@ -59,7 +61,7 @@ def main():
             ro, rf = int(m.group(1)), int(m.group(2))
             print("solve %2d  rounds/lane %.3f  refine/round %.3f" % (k, ro / S, rf / max(ro, 1)))
             k += 1
-        if line.startswith("[emu rescue"):
+        if line.startswith("[emu rescue") or line.startswith("[emu cold"):
             print("          " + line[:120])
     # -DPHX_EMU_REFINE_TRACE: per refinement solve, the sequence of relative corrections
     seqs, cur = [], []

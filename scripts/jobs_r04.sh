@@ -18,5 +18,9 @@ case "$1" in
   s3)  $J "test:tests/test_gpu_parity.py tests/test_trajectories.py tests/test_hydro.py" "bench:r04_s3_c3s8:$S8" \
           "bench:r04_s3_bench:$H" "prof:r04_s3_prof:$H --ar-probe 0" "prof:r04_s3_c3s8_prof:$S8" && \
        PHX_LANE_STAMPS=1 $J "bench:r04_s3_c3s8_stamps:$S8" "bench:r04_s3_stamps:$H --ar-probe 0" ;;
+  s4)  $J "test:tests/test_gpu_parity.py tests/test_trajectories.py tests/test_hydro.py tests/test_engine_emu.py" \
+          "bench:r04_s4_c3s8:$S8" "bench:r04_s4_bench:$H" "prof:r04_s4_prof:$H --ar-probe 0" "prof:r04_s4_c3s8_prof:$S8" && \
+       PHX_FZ_LEGACY=1 $J "bench:r04_s4_c3s8_legacy:$S8" "bench:r04_s4_bench_legacy:$H" && \
+       PHX_LANE_STAMPS=1 $J "bench:r04_s4_c3s8_stamps:$S8" "bench:r04_s4_stamps:$H --ar-probe 0" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
