@@ -42,7 +42,21 @@ struct LaneStructure {
     // as literals (c / lb,ub / bl,bu only when they do not vary across
     // scenarios); dc, dr: the generic path's column/row scaling
     std::vector<double> Ac, dc, dr, c, lb, ub, bl, bu;
+    // the interior point's start scales (lane_scales): primal offsets from the
+    // bounds / row sides, bound and row multipliers
+    double ipm_xs = 1.0, ipm_zs = 1.0, ipm_ws = 1.0;
 };
+
+// median of the nonzero finite magnitudes (0 if none)
+inline double median_mag(std::vector<double> v) {
+    std::vector<double> a;
+    for (double x : v)
+        if (std::isfinite(x) && x != 0.0) a.push_back(std::fabs(x));
+    if (a.empty()) return 0.0;
+    std::sort(a.begin(), a.end());
+    const size_t h = a.size() / 2;
+    return a.size() % 2 ? a[h] : 0.5 * (a[h - 1] + a[h]);
+}
 
 // Attach the scaled invariant numbers (host copies of the device arrays).
 inline void set_lane_values(LaneStructure& L, const std::vector<double>& Ac, const std::vector<double>& dc,
@@ -50,6 +64,14 @@ inline void set_lane_values(LaneStructure& L, const std::vector<double>& Ac, con
                             const std::vector<double>& lb, const std::vector<double>& ub,
                             const std::vector<double>& bl, const std::vector<double>& bu) {
     L.Ac = Ac; L.dc = dc; L.dr = dr;
+    // the multipliers' start scale from the costs (half their median
+    // magnitude; with scenario-varying costs the first scenario's)
+    {
+        std::vector<double> cc(c.begin(), c.begin() + std::min(c.size(), (size_t)L.n));
+        const double mc = median_mag(cc);
+        L.ipm_ws = mc > 0.0 ? std::min(std::max(0.5 * mc, 1e-3), 1e4) : 1.0;
+        L.ipm_zs = 0.1 * L.ipm_ws;
+    }
     L.c = L.c_vary ? std::vector<double>() : c;
     L.lb = L.bnd_vary ? std::vector<double>() : lb;
     L.ub = L.bnd_vary ? std::vector<double>() : ub;
@@ -137,6 +159,17 @@ inline bool build_lane_structure(const HostSetup& hs, int n, int m, int nnz, boo
             if ((bl[(size_t)s * m + i] == bu[(size_t)s * m + i]) != (bool)e) { why = "equality varies"; return false; }
         L.eq[i] = (uint8_t)e;
     }
+    // the primal start scale: a fifth of the median magnitude of the first
+    // scenario's finite bounds and row sides (interior-point iterations on the
+    // emulation, Iter0, wave-max mean: farmer 16.3 -> ~11, aircond 11.7 -> ~10;
+    // scripts/emu_ipm.py)
+    {
+        std::vector<double> v;
+        for (int j = 0; j < n; ++j) { v.push_back(lb[j]); v.push_back(ub[j]); }
+        for (int i = 0; i < m; ++i) { v.push_back(bl[i]); v.push_back(bu[i]); }
+        const double mp = median_mag(v);
+        L.ipm_xs = mp > 0.0 ? std::min(std::max(0.2 * mp, 1.0), 1e4) : 1.0;
+    }
     return true;
 }
 
@@ -185,6 +218,15 @@ inline std::string lane_kernel_source(const LaneStructure& L, int warm_waves = 1
       << "; }\n";
     o << "  __host__ __device__ static constexpr bool rhs_vary() { return " << (L.rhs_vary ? "true" : "false")
       << "; }\n";
+    {
+        char buf[160];
+        snprintf(buf, sizeof(buf), "  __host__ __device__ static constexpr double ipm_xs() { return %a; }\n", L.ipm_xs);
+        o << buf;
+        snprintf(buf, sizeof(buf), "  __host__ __device__ static constexpr double ipm_zs() { return %a; }\n", L.ipm_zs);
+        o << buf;
+        snprintf(buf, sizeof(buf), "  __host__ __device__ static constexpr double ipm_ws() { return %a; }\n", L.ipm_ws);
+        o << buf;
+    }
     emit_table(o, "int", "row", L.row);
     emit_table(o, "int", "col", L.col);
     emit_table(o, "int", "kvar", L.kvar);

@@ -530,10 +530,24 @@ PHX_LD void ipm_opaque(double* x, double* zl, double* zu, double* rl, double* ru
     }
 }
 
+// The start point's scales come from the problem (phx_jit.h: xs a fifth of
+// the median bound / row-side magnitude, ws half the median cost magnitude,
+// zs a tenth of ws); PHX_IPM_SCALES=0 (a JIT define) restores the unit
+// offsets of rounds 1-3.
+#if defined(PHX_IPM_SCALES) && PHX_IPM_SCALES == 0
+#define PHX_IPM_XS_ 1.0
+#define PHX_IPM_ZS_ 1.0
+#define PHX_IPM_WS_ 1.0
+#else
+#define PHX_IPM_XS_ PT::ipm_xs()
+#define PHX_IPM_ZS_ PT::ipm_zs()
+#define PHX_IPM_WS_ PT::ipm_ws()
+#endif
 template <class PT>
 PHX_LD double ipm_core(const Data<PT>& D, int max_it, double tol, double* x, double* y, int* its) {
     constexpr int NN = PT::NMAX_N, MM = PT::NMAX_M, TT = PT::NMAX_M * (PT::NMAX_M + 1) / 2;
     const double reg = 1e-10;
+    const double xs = PHX_IPM_XS_, zs = PHX_IPM_ZS_, ws = PHX_IPM_WS_;
     double zl[NN], zu[NN], s[MM], wl[MM], wu[MM];
     // start point (cost-aware multipliers)
     PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
@@ -541,13 +555,13 @@ PHX_LD double ipm_core(const Data<PT>& D, int max_it, double tol, double* x, dou
         if (PT::fixed(j)) xv = D.l(j);
         else if (PT::lfin(j) && PT::ufin(j)) {
             const double lo = D.l(j), hi = D.u(j);
-            xv = (hi - lo <= 2.0) ? 0.5 * (lo + hi) : clampd(0.0, lo + 1.0, hi - 1.0);
-        } else if (PT::lfin(j)) xv = fmax(0.0, D.l(j) + 1.0);
-        else if (PT::ufin(j)) xv = fmin(0.0, D.u(j) - 1.0);
+            xv = (hi - lo <= 2.0 * xs) ? 0.5 * (lo + hi) : clampd(0.0, lo + xs, hi - xs);
+        } else if (PT::lfin(j)) xv = fmax(0.0, D.l(j) + xs);
+        else if (PT::ufin(j)) xv = fmin(0.0, D.u(j) - xs);
         x[j] = xv;
         const double g = D.q(j) + D.p(j) * xv;
-        zl[j] = has_lo<PT>(j) ? fmax(g, 0.0) + 1.0 : 0.0;
-        zu[j] = has_up<PT>(j) ? fmax(-g, 0.0) + 1.0 : 0.0;
+        zl[j] = has_lo<PT>(j) ? fmax(g, 0.0) + zs : 0.0;
+        zu[j] = has_up<PT>(j) ? fmax(-g, 0.0) + zs : 0.0;
     }
     {
         double ax[MM];
@@ -557,12 +571,12 @@ PHX_LD double ipm_core(const Data<PT>& D, int max_it, double tol, double* x, dou
             if (PT::eq(i)) sv = D.bl(i);
             else if (PT::blfin(i) && PT::bufin(i)) {
                 const double lo = D.bl(i), hi = D.bu(i);
-                sv = (hi - lo <= 2.0) ? 0.5 * (lo + hi) : clampd(ax[i], lo + 1.0, hi - 1.0);
-            } else if (PT::blfin(i)) sv = fmax(ax[i], D.bl(i) + 1.0);
-            else if (PT::bufin(i)) sv = fmin(ax[i], D.bu(i) - 1.0);
+                sv = (hi - lo <= 2.0 * xs) ? 0.5 * (lo + hi) : clampd(ax[i], lo + xs, hi - xs);
+            } else if (PT::blfin(i)) sv = fmax(ax[i], D.bl(i) + xs);
+            else if (PT::bufin(i)) sv = fmin(ax[i], D.bu(i) - xs);
             s[i] = sv;
-            wl[i] = row_lo<PT>(i) ? 1.0 : 0.0;
-            wu[i] = row_up<PT>(i) ? 1.0 : 0.0;
+            wl[i] = row_lo<PT>(i) ? ws : 0.0;
+            wu[i] = row_up<PT>(i) ? ws : 0.0;
             y[i] = wl[i] - wu[i];
         }
     }
