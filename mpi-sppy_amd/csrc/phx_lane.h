@@ -54,6 +54,15 @@ typedef unsigned long long uint64_t;
 #define PHX_UNROLL
 #define PHX_NOUNROLL
 #endif
+// The interior point's predictor / corrector passes, unrolled: the
+// predictor's complementarity terms fold (no shift, no second-order term) --
+// 17 % fewer VALU instructions per interior-point iteration on farmer, 44 ->
+// 28 B of scratch (offline ISA, r04).  PHX_IPM_PASS_ROLLED keeps the loop.
+#ifdef PHX_IPM_PASS_ROLLED
+#define PHX_IPM_PASS_LOOP PHX_NOUNROLL
+#else
+#define PHX_IPM_PASS_LOOP PHX_UNROLL
+#endif
 // Refinement loop: kept as a loop by default (the fully unrolled refinement
 // multiplies the straight-line code the instruction cache must stream).
 #ifdef PHX_REFINE_UNROLL
@@ -632,7 +641,7 @@ PHX_LD double ipm_core(const Data<PT>& D, int max_it, double tol, double* x, dou
         double dx[NN], ds[MM], dy[MM], dxa[NN], dsa[MM];
         PHX_UNROLL for (int j = 0; j < PT::n(); ++j) dxa[j] = 0.0;
         PHX_UNROLL for (int i = 0; i < PT::m(); ++i) dsa[i] = 0.0;
-        PHX_NOUNROLL for (int pass = 0; pass < 2; ++pass) {
+        PHX_IPM_PASS_LOOP for (int pass = 0; pass < 2; ++pass) {
             ipm_opaque<PT>(x, zl, zu, rl, ru, s, wl, wu, rwl, rwu, y);
             {
                 double ax[MM], aty[NN];
