@@ -296,6 +296,16 @@ inline std::string lane_kernel_source(const LaneStructure& L, int warm_waves = 1
     o << "extern \"C\" __global__ void __launch_bounds__(64, 1) phx_lane_warm_fz1(phx_lane::LaneIO io) {\n"
          "  phx_lane::warm_fused<PT>(io);\n"
          "}\n";
+    // a whole warm solve (warm rounds, rescue rounds, interior point) in one
+    // launch, for batches of at most one wavefront per SIMD (phx_lane.h all_lane)
+    o << "extern \"C\" __global__ void __launch_bounds__(64, 1) phx_lane_all(phx_lane::LaneIO io, int rescue) {\n"
+         "  if (phx_lane::gated(io.gate)) return;\n"
+         "  phx_lane::zero_next_counts(io.counts_next);\n"
+         "  const int t = blockIdx.x * 64 + threadIdx.x;\n"
+         "  bool still = false;\n"
+         "  if (t < io.S) still = phx_lane::all_lane<PT>(io, t, rescue);\n"
+         "  phx_lane::compact_lane(still, t, io.lanes_out, io.count_out);\n"
+         "}\n";
     // phx_iterk fused mode, after the last enqueued iteration: the decision on
     // its conv (the next warm launch's prologue does it otherwise)
     o << "extern \"C\" __global__ void __launch_bounds__(64) phx_fz_tail(phx_lane::LaneIO io) {\n"

@@ -848,21 +848,38 @@ PHX_LD void aset_load(const LaneIO& io, int sc, ASet<PT>& a) {
 // the active set from its stored words (2 bits per column, then per row)
 template <class PT>
 PHX_LD void aset_from_words(const uint32_t* w, ASet<PT>& a) {
+    // (0/1 integers, vbit: no per-lane bool held live)
+    typedef typename ASet<PT>::CMask CM;
+    CM fw = 0, uw = 0;
+    uint32_t rw = 0, lw = 0;
     PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
         const uint32_t v = (w[(2 * j) >> 5] >> ((2 * j) & 31)) & 3u;
-        bool fr = !PT::fixed(j) && v == 0u;
-        bool upj = !PT::fixed(j) && v == 2u;
-        if (upj && !PT::ufin(j)) { upj = false; fr = true; }
-        if (!fr && !upj && !PT::lfin(j) && !PT::fixed(j)) fr = true;
-        a.setF(j, fr);
-        a.setUp(j, upj);
+        uint32_t fr = 0u, upj = 0u;
+        if (!PT::fixed(j)) {
+            fr = vbit(v == 0u);
+            upj = vbit(v == 2u);
+            if (!PT::ufin(j)) { fr |= upj; upj = 0u; }              // at an infinite upper bound: free
+            if (!PT::lfin(j)) fr |= (fr | upj) ^ 1u;                 // at an infinite lower bound: free
+        }
+        fw |= (CM)fr << j;
+        uw |= (CM)upj << j;
     }
     PHX_UNROLL for (int i = 0; i < PT::m(); ++i) {
         const int b = 2 * (PT::n() + i);
         const uint32_t v = (w[b >> 5] >> (b & 31)) & 3u;
-        a.setR(i, PT::eq(i) || (v == 1u && PT::blfin(i)) || (v == 2u && PT::bufin(i)));
-        a.setLo(i, PT::eq(i) || v == 1u);
+        uint32_t R, L;
+        if (PT::eq(i)) { R = 1u; L = 1u; }
+        else {
+            L = vbit(v == 1u);
+            R = (PT::blfin(i) ? L : 0u) | (PT::bufin(i) ? vbit(v == 2u) : 0u);
+        }
+        rw |= R << i;
+        lw |= L << i;
     }
+    a.f = fw;
+    a.u = uw;
+    a.r = rw;
+    a.l = lw;
 }
 
 template <class PT>
@@ -890,37 +907,46 @@ PHX_LD void aset_store(const LaneIO& io, int sc, const ASet<PT>& a) {
 // (OSQP's polish rule, sharp at IPM points by strict complementarity).
 template <class PT>
 PHX_LD void classify(const Data<PT>& D, const double* xv, const double* yv, double tol, ASet<PT>& a) {
+    // (the words built from 0/1 integers, vbit: no per-lane bool held live)
+    typedef typename ASet<PT>::CMask CM;
+    CM fw = 0, uw = 0;
+    uint32_t rw = 0, lw = 0;
     double aty[PT::NMAX_N];
     D.matvec_t(yv, aty);
     PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
         const double lam = D.qpx(j, xv[j]) - aty[j];
-        bool fr = !PT::fixed(j), upj = false;
-        if (fr && PT::lfin(j)) {
+        uint32_t fr = PT::fixed(j) ? 0u : 1u, upj = 0u;
+        if (PT::lfin(j)) {
             const double lo = D.l(j);
-            if (xv[j] - lo <= tol * (1.0 + fabs(lo)) || xv[j] - lo < lam) fr = false;
+            fr &= vbit(xv[j] - lo <= tol * (1.0 + fabs(lo)) || xv[j] - lo < lam) ^ 1u;
         }
-        if (fr && PT::ufin(j)) {
+        if (PT::ufin(j)) {
             const double hi = D.u(j);
-            if (hi - xv[j] <= tol * (1.0 + fabs(hi)) || hi - xv[j] < -lam) { fr = false; upj = true; }
+            upj = fr & vbit(hi - xv[j] <= tol * (1.0 + fabs(hi)) || hi - xv[j] < -lam);
+            fr &= upj ^ 1u;
         }
-        a.setF(j, fr);
-        a.setUp(j, upj);
+        fw |= (CM)fr << j;
+        uw |= (CM)upj << j;
     }
     double ax[PT::NMAX_M];
     D.matvec(xv, ax);
     PHX_UNROLL for (int i = 0; i < PT::m(); ++i) {
-        bool lo_act = PT::eq(i), up_act = false;
-        if (!lo_act && PT::blfin(i)) {
+        uint32_t lo_act = PT::eq(i) ? 1u : 0u, up_act = 0u;
+        if (!PT::eq(i) && PT::blfin(i)) {
             const double lo = D.bl(i);
-            lo_act = ax[i] - lo <= tol * (1.0 + fabs(lo)) || ax[i] - lo < yv[i];
+            lo_act = vbit(ax[i] - lo <= tol * (1.0 + fabs(lo)) || ax[i] - lo < yv[i]);
         }
-        if (!lo_act && PT::bufin(i)) {
+        if (!PT::eq(i) && PT::bufin(i)) {
             const double hi = D.bu(i);
-            up_act = hi - ax[i] <= tol * (1.0 + fabs(hi)) || hi - ax[i] < -yv[i];
+            up_act = (lo_act ^ 1u) & vbit(hi - ax[i] <= tol * (1.0 + fabs(hi)) || hi - ax[i] < -yv[i]);
         }
-        a.setR(i, lo_act || up_act);
-        a.setLo(i, lo_act);
+        rw |= (lo_act | up_act) << i;
+        lw |= lo_act << i;
     }
+    a.f = fw;
+    a.u = uw;
+    a.r = rw;
+    a.l = lw;
 }
 
 // Equality-constrained KKT solve for the active set a:
@@ -1597,6 +1623,29 @@ PHX_LD bool cold_rounds_lane(const LaneIO& io, int sc) {
     // finish_lane); a converged one whose rounds failed is not repeated
     if (!(err < 1e-4)) io.flags[sc] = 0;
     return true;
+}
+
+// The whole warm solve of one lane in one kernel (phx_lane_all), for
+// batches of at most one wavefront per SIMD, where every pass is one
+// wavefront's latency whatever its lane count: the warm rounds, then on the
+// lanes they leave the rescue rounds (single changes from the updated active
+// set), then the interior point and its rounds -- the same per-lane functions
+// in the same order as the warm, rescue-list and cold passes, so the same
+// results, in one launch instead of four (three of them usually empty).
+// true: the lane needs the generic path.
+template <class PT>
+PHX_LD bool all_lane(const LaneIO& io, int sc, int rescue) {
+    if (!warm_lane<PT, false>(io, sc)) return false;
+    if (rescue > 0) {
+        LaneIO io2 = io;
+        io2.warm_rounds = rescue;
+        io2.single_after = 1;
+        if (!warm_lane<PT, false>(io2, sc)) return false;
+    }
+    LaneIO io3 = io;
+    io3.single_after = 1;          // (the cold pass after warm passes: single changes, phx_kernels.hip)
+    ipm_lane<PT>(io3, sc);
+    return cold_rounds_lane<PT>(io3, sc);
 }
 
 // Both halves for one lane (the host emulation; the GPU runs them as two
