@@ -420,7 +420,16 @@ def dominant_kernel(ph, K, fused):
         # launch, or (subproblems above the lane limits) the workgroup pass
         info = ph._native.jit_info(ph._ctx).decode()
         if info.startswith("on"):
-            return ("phx_lane_warm", st["lane_warm_ms"] / 1e3 / st["warm_launches"], st["warm_launches"],
+            # the lane kernel that ran (phx_kernels.hip enqueue_lane_solve): the
+            # fused iteration kernel (its one-wave-per-SIMD build for batches of
+            # at most one wavefront per SIMD), or unfused (multistage) the one-launch
+            # small-batch solve / the warm pass
+            small = -(-b.S // 64) <= simds()
+            if st.get("fused"):
+                kname = "phx_lane_warm_fz1" if small else "phx_lane_warm_fz"
+            else:
+                kname = "phx_lane_all" if small else "phx_lane_warm"
+            return (kname, st["lane_warm_ms"] / 1e3 / st["warm_launches"], st["warm_launches"],
                     lane_bytes(b, fused=bool(st.get("fused")) and fused), b.S)
         if "workgroup solver on" in info:
             return ("k_wg_warm", st["lane_warm_ms"] / 1e3 / st["warm_launches"], st["warm_launches"], wg_bytes(b),
@@ -445,6 +454,14 @@ def dominant_kernel(ph, K, fused):
         if cert and any(s.get("wg_ms", 0.0) > 0.0 for s in stats):
             units = max(1, int(np.mean(cert)))
     return name, ms / 1e3 / max(launches, 1), launches, bpu, units
+
+
+def simds():
+    """SIMDs of the GPU (4 per CU), the lane kernels' one-wave slots."""
+    try:
+        return 4 * torch.cuda.get_device_properties(0).multi_processor_count
+    except Exception:
+        return 1024
 
 
 def roofline(kernel, avg_s, launches, bpu, units, traffic=None, traffic_src=None, traffic_status=None):
@@ -575,7 +592,7 @@ def main():
         "T_s": T, "iter0_s": T0,
         "steady": {"value": S * K / Tk, "ms_per_step": Tk * 1e3 / K, "def": "S K / T_iterk (Iter0 excluded)"},
         "roofline": dict(roofline(kernel, avg_s, launches, bpu, units, traffic, tsrc, tstat),
-                         valu=valu_issue(kernel, "farmer100k", units, avg_s)
+                         valu=valu_issue(kernel, "farmer100k", units, avg_s, simds=simds())
                          if (world == 1 and args.only is None and S == 100000 and cm == 1) else None),
         "loop": ("PHBase.iterk_loop -> phx_iterk (device-driven, depth %d%s)"
                  % (args.depth, ", fused" if st and st.get("fused") else "")) if st else "PHBase host loop",

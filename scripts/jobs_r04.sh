@@ -22,5 +22,14 @@ case "$1" in
           "bench:r04_s4_c3s8:$S8" "bench:r04_s4_bench:$H" "prof:r04_s4_prof:$H --ar-probe 0" "prof:r04_s4_c3s8_prof:$S8" && \
        PHX_FZ_LEGACY=1 $J "bench:r04_s4_c3s8_legacy:$S8" "bench:r04_s4_bench_legacy:$H" && \
        PHX_LANE_STAMPS=1 $J "bench:r04_s4_c3s8_stamps:$S8" "bench:r04_s4_stamps:$H --ar-probe 0" ;;
+  pmc) # PMC passes on the final kernels (one counter group per pass): FETCH_SIZE, WRITE_SIZE per config,
+       # the SQ instruction / wait counters for the headline and the per-rank slice
+       $J "pmc:r04_pmc_c3_fetch:FETCH_SIZE:$B" "pmc:r04_pmc_c3_write:WRITE_SIZE:$B" "pmc:r04_pmc_c3_sq:$SQ:$B" \
+          "pmc:r04_pmc_s8_fetch:FETCH_SIZE:$S8" "pmc:r04_pmc_s8_write:WRITE_SIZE:$S8" "pmc:r04_pmc_s8_sq:$SQ:$S8" \
+          "pmc:r04_pmc_1m_fetch:FETCH_SIZE:$M" "pmc:r04_pmc_1m_write:WRITE_SIZE:$M" \
+          "pmc:r04_pmc_c2_fetch:FETCH_SIZE:--only C2 $A" "pmc:r04_pmc_c2_write:WRITE_SIZE:--only C2 $A" \
+          "pmc:r04_pmc_c4_fetch:FETCH_SIZE:--only C4 $A" "pmc:r04_pmc_c4_write:WRITE_SIZE:--only C4 $A" \
+          "pmc:r04_pmc_c5a_fetch:FETCH_SIZE:--only C5a $A" "pmc:r04_pmc_c5a_write:WRITE_SIZE:--only C5a $A" \
+          "pmc:r04_pmc_c5b_fetch:FETCH_SIZE:--only C5b $A" "pmc:r04_pmc_c5b_write:WRITE_SIZE:--only C5b $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac

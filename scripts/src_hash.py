@@ -9,8 +9,9 @@ import os
 _ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 _CSRC = os.path.join(_ROOT, "mpi-sppy_amd", "csrc")
 # phx_kernels.hip holds every launch (grids, options, the loop): part of each set
+_LANE = ["phx_lane.h", "phx_jit.h", "phx_setup.h", "phx_kernels.hip"]
 KERNEL_SOURCES = {
-    "phx_lane_warm": ["phx_lane.h", "phx_jit.h", "phx_setup.h", "phx_kernels.hip"],
+    "phx_lane_warm": _LANE, "phx_lane_warm_fz": _LANE, "phx_lane_warm_fz1": _LANE, "phx_lane_all": _LANE,
     "k_wg_warm": ["phx_wg.h", "phx_core.h", "phx_setup.h", "phx_kernels.hip"],
     "k_sp_solve": ["phx_sp.h", "phx_core.h", "phx_setup.h", "phx_kernels.hip"],
 }

@@ -57,10 +57,16 @@ def check_hub(lib, device, S=12, iters=4):
     N = ph.batch.nonant.N
     assert np.array_equal(hub.w_bufs[-1][:S * N], ph.W_array().ravel())
     assert np.array_equal(hub.nonant_bufs[-1], ph.nonant_values().ravel())
-    # the same trajectory as without a hub
-    ref = PH(ph_options(iters), names, farmer.scenario_creator, scenario_creator_kwargs={"num_scens": S},
+    # the same trajectory as without a hub, bit for bit: the same host loop
+    # (without a hub ph_main would run the device loop, whose fused reductions
+    # sum in another fixed order -- agreement to 1e-9 there, tested in
+    # test_native_loop_fused_matches_host_loop_gpu)
+    ropts = ph_options(iters)
+    ropts["iterk_solver_options"] = {"native_loop": 0}
+    ref = PH(ropts, names, farmer.scenario_creator, scenario_creator_kwargs={"num_scens": S},
              _native_lib=lib, _device=device)
     rc, rE, rt = ref.ph_main()
+    assert not hasattr(ref, "iterk_stats")
     assert np.array_equal(ref.W_array(), ph.W_array()) and rc == conv and rt == tb
     # is_converged ends iterk_loop right after the solve of that iteration
     ph2 = PH(ph_options(iters), names, farmer.scenario_creator, scenario_creator_kwargs={"num_scens": S},
