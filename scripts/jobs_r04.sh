@@ -22,6 +22,11 @@ case "$1" in
           "bench:r04_s4_c3s8:$S8" "bench:r04_s4_bench:$H" "prof:r04_s4_prof:$H --ar-probe 0" "prof:r04_s4_c3s8_prof:$S8" && \
        PHX_FZ_LEGACY=1 $J "bench:r04_s4_c3s8_legacy:$S8" "bench:r04_s4_bench_legacy:$H" && \
        PHX_LANE_STAMPS=1 $J "bench:r04_s4_c3s8_stamps:$S8" "bench:r04_s4_stamps:$H --ar-probe 0" ;;
+  s5)  # the workgroup solver's factor cache, pay or drop; its phase clocks; the default command
+       $J "bench:r04_s5_c2:--only C2 $A" "bench:r04_s5_c5a:--only C5a $A" "prof:r04_s5_c4_prof:--only C4 $A" && \
+       PHX_WG_NO_FACTOR_CACHE=1 $J "bench:r04_s5_c2_nocache:--only C2 $A" "bench:r04_s5_c5a_nocache:--only C5a $A" && \
+       PHX_WG_PROF=1 $J "bench:r04_s5_c2_wgprof:--only C2 $A" "bench:r04_s5_c5a_wgprof:--only C5a $A" && \
+       $J "bench:r04_s5_default:" ;;
   pmc) # PMC passes on the final kernels (one counter group per pass): FETCH_SIZE, WRITE_SIZE per config,
        # the SQ instruction / wait counters for the headline and the per-rank slice
        $J "pmc:r04_pmc_c3_fetch:FETCH_SIZE:$B" "pmc:r04_pmc_c3_write:WRITE_SIZE:$B" "pmc:r04_pmc_c3_sq:$SQ:$B" \
