@@ -27,6 +27,8 @@ case "$1" in
        PHX_WG_NO_FACTOR_CACHE=1 $J "bench:r04_s5_c2_nocache:--only C2 $A" "bench:r04_s5_c5a_nocache:--only C5a $A" && \
        PHX_WG_PROF=1 $J "bench:r04_s5_c2_wgprof:--only C2 $A" "bench:r04_s5_c5a_wgprof:--only C5a $A" && \
        $J "bench:r04_s5_default:" ;;
+  s6)  # host launch calls against device starts (the loop's dispatch gaps)
+       $J "trace:r04_s6_c3s8_trace:$S8" "trace:r04_s6_trace:$H --ar-probe 0" ;;
   pmc) # PMC passes on the final kernels (one counter group per pass): FETCH_SIZE, WRITE_SIZE per config,
        # the SQ instruction / wait counters for the headline and the per-rank slice
        $J "pmc:r04_pmc_c3_fetch:FETCH_SIZE:$B" "pmc:r04_pmc_c3_write:WRITE_SIZE:$B" "pmc:r04_pmc_c3_sq:$SQ:$B" \
