@@ -70,8 +70,10 @@ def parse():
     ap.add_argument("--lane-solver", type=int, default=1, help="1: structure-specialised lane solver first")
     ap.add_argument("--depth", type=int, default=4, help="phx_iterk: iterations kept enqueued ahead")
     ap.add_argument("--fused", type=int, default=1, help="phx_iterk: one launch per PH iteration")
-    ap.add_argument("--timing-every", type=int, default=5,
-                    help="phx_iterk: HIP events around the lane kernel of every T-th iteration")
+    ap.add_argument("--timing-every", type=int, default=-5,
+                    help="phx_iterk: T > 0: HIP events around the lane kernel of every T-th iteration; "
+                         "T < 0: fused loop: one event pair around all its launches (back to back: no "
+                         "per-launch event records in the timed loop), unfused: every |T|-th")
     ap.add_argument("--no-conv", action="store_true", help="skip time to conv < 1e-4")
     ap.add_argument("--conv-max-iters", type=int, default=10000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -473,7 +475,14 @@ def roofline(kernel, avg_s, launches, bpu, units, traffic=None, traffic_src=None
             "traffic_ratio": (traffic / bytes_per_launch) if (traffic and bytes_per_launch) else None,
             "algorithmic_bytes_per_launch": bytes_per_launch, "kernel": kernel,
             "bytes_per_unit": bpu, "unit_def": "scenario solve", "units_per_launch": units,
-            "avg_launch_us": avg_s * 1e6, "launches": launches}
+            "avg_launch_us": avg_s * 1e6, "launches": launches,
+            "launch_timing": LAUNCH_TIMING.get(kernel, "HIP events around sampled launches")}
+
+
+# how phx_iterk's events time the dominant kernel (bench --timing-every < 0)
+LAUNCH_TIMING = {k: ("one HIP event pair around all the fused launches of the timed loop (back to back on "
+                     "phx_iterk's stream; no per-launch records in between)")
+                 for k in ("phx_lane_warm_fz", "phx_lane_warm_fz1")}
 
 
 def run_config(name, w, args, K, so, world, dev):

@@ -317,7 +317,11 @@ typedef struct phx_iterk_args {
     int32_t depth;                   /* iterations kept enqueued ahead (>= 1)    */
     int32_t timing;                  /* T > 0: HIP events around the phx_lane_warm launch of
                                         every T-th iteration (each record costs ~6 us of GPU
-                                        time, so the sample is sparse); 0: none            */
+                                        time, so the sample is sparse); 0: none; T < 0: one
+                                        event pair around ALL the fused launches of a run that
+                                        reaches max_iters without a stop (back to back, so
+                                        the window is their summed durations; unfused modes:
+                                        every |T|-th iteration as T > 0)                   */
     phx_allreduce_fn allreduce;      /* NULL on one rank                         */
     void* allreduce_user;
     int32_t node_stage_len;          /* doubles in node_stage; >= 2*NNS+1+conv_R enables the

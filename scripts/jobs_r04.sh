@@ -31,6 +31,9 @@ case "$1" in
        $J "trace:r04_s6_c3s8_trace:$S8" "trace:r04_s6_trace:$H --ar-probe 0" ;;
   s7)  # the poll without stream queries: the fused loop's dispatch gaps
        $J "bench:r04_s7_c3s8:$S8" "bench:r04_s7_bench:$H" "trace:r04_s7_c3s8_trace:$S8" "trace:r04_s7_trace:$H --ar-probe 0" ;;
+  s8)  # window timing of the fused launches (no event records inside the loop)
+       $J "test:tests/test_gpu_parity.py -k window_timing" "bench:r04_s8_c3s8:$S8" "bench:r04_s8_bench:$H" \
+          "prof:r04_s8_c3s8_prof:$S8" "prof:r04_s8_prof:$H --ar-probe 0" ;;
   pmc) # PMC passes on the final kernels (one counter group per pass): FETCH_SIZE, WRITE_SIZE per config,
        # the SQ instruction / wait counters for the headline and the per-rank slice
        $J "pmc:r04_pmc_c3_fetch:FETCH_SIZE:$B" "pmc:r04_pmc_c3_write:WRITE_SIZE:$B" "pmc:r04_pmc_c3_sq:$SQ:$B" \

@@ -488,3 +488,18 @@ def test_split_layouts_bit_equal_gpu(gpu_lib, monkeypatch, env, creator_kw):
     assert np.array_equal(out["0"][0], out["1"][0])
     assert np.array_equal(out["0"][1], out["1"][1])
     assert out["0"][2] == out["1"][2] and out["0"][3] == out["1"][3]
+
+
+def test_window_timing_fused_loop_gpu(gpu_lib):
+    """iterk_timing < 0 (bench.py's default): one event pair around every fused
+    launch of the run (iteration 1 after Iter0 is the unfused rescue iteration,
+    so iterations 2..K), and the same trajectory as the untimed loop."""
+    S, K = 1000, 10
+    names = farmer.scenario_names_creator(S)
+    a, _, _, _ = run_engine(farmer.scenario_creator, names, {"num_scens": S}, K, lib=gpu_lib,
+                            options={"iterk_solver_options": {"iterk_timing": -5}})
+    b, _, _, _ = run_engine(farmer.scenario_creator, names, {"num_scens": S}, K, lib=gpu_lib)
+    st = a.iterk_stats
+    assert st["fused"] and st["iters"] == K
+    assert st["warm_launches"] == K - 1 and st["lane_warm_ms"] > 0.0
+    assert np.array_equal(a.W_array(), b.W_array())
