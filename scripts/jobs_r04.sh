@@ -34,6 +34,8 @@ case "$1" in
   s8)  # window timing of the fused launches (no event records inside the loop)
        $J "test:tests/test_gpu_parity.py -k window_timing" "bench:r04_s8_c3s8:$S8" "bench:r04_s8_bench:$H" \
           "prof:r04_s8_c3s8_prof:$S8" "prof:r04_s8_prof:$H --ar-probe 0" ;;
+  s9)  # the workgroup solver's phase clocks in the device loop
+       PHX_WG_PROF=1 $J "bench:r04_s9_c2_wgprof:--only C2 $A" "bench:r04_s9_c5a_wgprof:--only C5a $A" ;;
   pmc) # PMC passes on the final kernels (one counter group per pass): FETCH_SIZE, WRITE_SIZE per config,
        # the SQ instruction / wait counters for the headline and the per-rank slice
        $J "pmc:r04_pmc_c3_fetch:FETCH_SIZE:$B" "pmc:r04_pmc_c3_write:WRITE_SIZE:$B" "pmc:r04_pmc_c3_sq:$SQ:$B" \
