@@ -36,6 +36,9 @@ case "$1" in
           "prof:r04_s8_c3s8_prof:$S8" "prof:r04_s8_prof:$H --ar-probe 0" ;;
   s9)  # the workgroup solver's phase clocks in the device loop
        PHX_WG_PROF=1 $J "bench:r04_s9_c2_wgprof:--only C2 $A" "bench:r04_s9_c5a_wgprof:--only C5a $A" ;;
+  s10) # the 1M configuration's loop (r04 s5: 10.9 ms per iteration, unfused)
+       PHX_ITERK_DEBUG=1 $J "bench:r04_s10_1m:--only C3x1M --no-cpu-baseline --no-conv --steps 10 --warmup 1" && \
+       PHX_QUERY_MS=0 $J "bench:r04_s10_1m_q0:--only C3x1M --no-cpu-baseline --no-conv --steps 10 --warmup 1" ;;
   pmc) # PMC passes on the final kernels (one counter group per pass): FETCH_SIZE, WRITE_SIZE per config,
        # the SQ instruction / wait counters for the headline and the per-rank slice
        $J "pmc:r04_pmc_c3_fetch:FETCH_SIZE:$B" "pmc:r04_pmc_c3_write:WRITE_SIZE:$B" "pmc:r04_pmc_c3_sq:$SQ:$B" \
