@@ -390,6 +390,14 @@ int phx_iterk_prepare(phx_ctx* ctx, const phx_iterk_args* args);
  * context ("on: ..." or "off: <reason>").                                   */
 const char* phx_jit_info(const phx_ctx* ctx);
 
+/* Test hook (no reference counterpart): the workgroup solver's Schur
+ * complement inverse (phx_wg.h wg_blk_cholesky -> wg_blk_trtri ->
+ * wg_blk_lauum, one 256-thread workgroup, the matrix in LDS) on one
+ * symmetric matrix s_host [ma x ma] (lower triangle read), ma <= 64.
+ * inv_host [ma x ma] receives the inverse; returns 1 if a pivot was not
+ * positive, 0 on success, -1 on a HIP error.                               */
+int phx_debug_spd_inverse(const double* s_host, int32_t ma, double* inv_host);
+
 #ifdef __cplusplus
 }
 #endif

@@ -100,7 +100,7 @@ class IterkResult(ctypes.Structure):
 SYMBOLS = [
     "create", "destroy", "last_error", "build_info", "set_problem", "set_bounds", "set_ph_terms",
     "solve", "solve_finish", "objective", "xbar", "update_w", "expect", "export_slots", "last_solve_stats", "jit_info",
-    "iterk", "iterk_prepare", "comm_unique_id", "set_comm",
+    "iterk", "iterk_prepare", "comm_unique_id", "set_comm", "debug_spd_inverse",
 ]
 
 
@@ -154,6 +154,7 @@ class Lib:
         self.iterk_prepare = fn("iterk_prepare", ctypes.c_int, [c_void_p, ctypes.POINTER(IterkArgs)])
         self.comm_unique_id = fn("comm_unique_id", ctypes.c_int, [c_void_p])
         self.set_comm = fn("set_comm", ctypes.c_int, [c_void_p, c_void_p, c_int32, c_int32])
+        self.debug_spd_inverse = fn("debug_spd_inverse", ctypes.c_int, [c_void_p, c_int32, c_void_p])
 
     def check(self, ctx, rc, what):
         if rc != 0:

@@ -238,9 +238,296 @@ PHX_HD void wg_compact(const WgLds& L, int m) {
 #endif
 }
 
+// ---- The Schur complement's inverse with f64 MFMA tiles (round 4) ----
+// Blocked versions of the three steps, in 16 x 16 blocks (rows and columns
+// past ma read as zero, never stored), for a Schur complement of at most
+// WG_BLK_MAX rows:
+//   wg_blk_cholesky: right-looking Cholesky; per panel the diagonal block is
+//     factored by wavefront 0 in registers, the rows below by forward
+//     substitution (a thread per row), and the trailing update
+//     W_IJ -= L_IP L_JP^T is MFMA.  Output as the scalar factor's: L[i][k]
+//     (i > k) at Sm[k*ld + i] (the upper part), 1 / L[k][k] in dg; the lower
+//     part is the working matrix.
+//   wg_blk_trtri: X = L^-1 into the lower part (diagonal included): diagonal
+//     blocks by a thread per column, then block row by block row
+//     X_IJ = -X_II sum_K L_IK X_KJ (MFMA).
+//   wg_blk_lauum: M^-1 = X^T X, the full symmetric matrix (MFMA), so that a
+//     refinement step is ONE dense mat-vec.
+// v_mfma_f64_16x16x4_f64 (MI355X_MICROARCH / cdna_hip_programming: lane l holds
+// A[l&15][k = 4s + (l>>4)] and B[k][l&15] of k-step s; C/D rows (l>>4) + 4r,
+// column l&15 of register r -- so a C tile's register s is the B operand of
+// k-step s of a following product).  The numbers are the scalar algorithms'
+// in another summation order (stable as they are: an in-place Gauss-Jordan
+// inverse was tried first and lost 20 digits on the degenerate faces'
+// nearly singular complements).
+#define WG_TB 16
+#define WG_BLK_MAX 64    // 4 x 4 blocks: wg_blk_lauum keeps a wavefront's tiles in registers
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef double wg_d4 __attribute__((ext_vector_type(4)));
+
+// Sm[r*ld + c] when r, c < ma (and, with `lower`, r >= c), else 0; a clamped
+// address (no read outside the matrix)
+__device__ __forceinline__ double wg_el(const double* Sm, int ld, int ma, int r, int c, bool lower = false) {
+    const bool in = r < ma && c < ma && (!lower || r >= c);
+    const double v = Sm[(in ? r : 0) * ld + (in ? c : 0)];
+    return in ? v : 0.0;
+}
+
+__device__ __forceinline__ double wg_readlane64(double v, int lane) {
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u & 0xffffffffull), lane);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), lane);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+#define WG_MFMA(a, b, c) __builtin_amdgcn_mfma_f64_16x16x4f64((a), (b), (c), 0, 0, 0)
+
+// Panel p0's diagonal block (wavefront 0; lane (r, g) = (l&15, l>>4) holds row
+// r, columns 4g..4g+3): Cholesky in registers (row / column broadcasts by lane
+// permutes), stored as L^T in the upper part and 1/L_jj in dg.  false
+// (uniform): a pivot is not positive.
+__device__ bool wg_blk_diag(double* Sm, int ld, int ma, int p0, double* dg) {
+    const int l = (int)(threadIdx.x & 63), r = l & 15, g = l >> 4;
+    const int w = ma - p0 < WG_TB ? ma - p0 : WG_TB;
+    double a[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int c = 4 * g + q;
+        const bool in = r < w && c < w && c <= r;
+        const double v = Sm[(p0 + (in ? r : 0)) * ld + p0 + (in ? c : 0)];
+        a[q] = in ? v : (r == c ? 1.0 : 0.0);
+    }
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < WG_TB; ++j) {
+        const double colj = a[j & 3];     // column j's slot, before this step changes it
+        const double d = wg_readlane64(colj, j + 16 * (j >> 2));    // a_jj
+        ok = ok && d > 0.0;
+        const double isd = 1.0 / sqrt(d);
+        const double lrj = __shfl(colj, r + 16 * (j >> 2), 64) * isd;   // L_rj (r >= j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int c = 4 * g + q;
+            const double lcj = __shfl(colj, c + 16 * (j >> 2), 64) * isd;   // L_cj (c >= j)
+            if (c == j) a[q] = lrj;
+            else if (c > j && c <= r) a[q] = fma(-lrj, lcj, a[q]);
+        }
+    }
+    // L[r][c] (r > c) at Sm[(p0+c)*ld + p0+r]; 1/L_rr in dg
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int c = 4 * g + q;
+        if (r < w && c < w) {
+            if (c < r) Sm[(p0 + c) * ld + p0 + r] = a[q];
+            else if (c == r) dg[p0 + r] = 1.0 / a[q];
+        }
+    }
+    return ok;
+}
+
+PHX_HD bool wg_blk_cholesky(double* Sm, int ld, int ma, double* dg, int32_t* flag) {
+    const int nb = (ma + WG_TB - 1) / WG_TB;
+    const int l = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6), r16 = l & 15, g = l >> 4;
+    for (int P = 0; P < nb; ++P) {
+        const int p0 = WG_TB * P, w = ma - p0 < WG_TB ? ma - p0 : WG_TB;
+        if (threadIdx.x < 64) {
+            const bool ok = wg_blk_diag(Sm, ld, ma, p0, dg);
+            if (!ok && threadIdx.x == 0) *flag = 1;
+        }
+        __syncthreads();
+        if (*flag) return false;
+        if (P + 1 == nb) break;
+        // rows below: L[i][p0+j] = (W[i][p0+j] - sum_{k<j} L[i][p0+k] L[p0+j][p0+k]) / L_jj
+        for (int i = p0 + WG_TB + (int)threadIdx.x; i < ma; i += WG_NT) {
+            double x[WG_TB];
+#pragma unroll
+            for (int j = 0; j < WG_TB; ++j) {
+                if (j < w) {
+                    double v = Sm[i * ld + p0 + j];
+#pragma unroll
+                    for (int k = 0; k < j; ++k) v = fma(-x[k], Sm[(p0 + k) * ld + p0 + j], v);
+                    x[j] = v * dg[p0 + j];
+                    Sm[(p0 + j) * ld + i] = x[j];
+                }
+            }
+        }
+        __syncthreads();
+        // trailing update of the lower tiles (I >= J > P), a tile per wavefront in turn
+        const int nt = nb - P - 1, ntile = nt * (nt + 1) / 2;
+        for (int t = wv; t < ntile; t += WG_NT / 64) {
+            int I = 0;
+            while ((I + 1) * (I + 2) / 2 <= t) ++I;
+            const int J = t - I * (I + 1) / 2;
+            const int I0 = WG_TB * (P + 1 + I), J0 = WG_TB * (P + 1 + J);
+            wg_d4 acc;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[q] = wg_el(Sm, ld, ma, I0 + g + 4 * q, J0 + r16);
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int kc = p0 + 4 * s + g;     // panel column k (its L^T row in the upper part)
+                const double av = (kc < p0 + w) ? -wg_el(Sm, ld, ma, kc, I0 + r16) : 0.0;
+                const double bv = (kc < p0 + w) ? wg_el(Sm, ld, ma, kc, J0 + r16) : 0.0;
+                acc = WG_MFMA(av, bv, acc);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int ri = I0 + g + 4 * q, cj = J0 + r16;
+                if (ri < ma && cj < ma && cj <= ri) Sm[ri * ld + cj] = acc[q];
+            }
+        }
+        __syncthreads();
+    }
+    return true;
+}
+
+// X = L^-1 (lower part, diagonal included) from wg_blk_cholesky's output
+PHX_HD void wg_blk_trtri(double* Sm, int ld, int ma, const double* dg) {
+    const int nb = (ma + WG_TB - 1) / WG_TB;
+    const int l = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6), r16 = l & 15, g = l >> 4;
+    // diagonal blocks: a thread per (block, column c): X[c][c] = 1/L_cc,
+    // X[i][c] = -(sum_{k=c}^{i-1} L[i][k] X[k][c]) / L_ii
+    for (int e = (int)threadIdx.x; e < nb * WG_TB; e += WG_NT) {
+        const int p0 = (e >> 4) * WG_TB, c = e & 15;
+        const int w = ma - p0 < WG_TB ? ma - p0 : WG_TB;
+        if (c >= w) continue;
+        double x[WG_TB];
+#pragma unroll
+        for (int i = 0; i < WG_TB; ++i) {
+            if (i < c || i >= w) continue;
+            if (i == c) {
+                x[i] = dg[p0 + c];
+            } else {
+                double v = 0.0;
+#pragma unroll
+                for (int k = 0; k < i; ++k)
+                    if (k >= c) v = fma(Sm[(p0 + k) * ld + p0 + i], x[k], v);
+                x[i] = -v * dg[p0 + i];
+            }
+            Sm[(p0 + i) * ld + p0 + c] = x[i];
+        }
+    }
+    __syncthreads();
+    for (int I = 1; I < nb; ++I) {
+        const int I0 = WG_TB * I;
+        for (int J = wv; J < I; J += WG_NT / 64) {
+            const int J0 = WG_TB * J;
+            wg_d4 tt = {0.0, 0.0, 0.0, 0.0};
+            for (int K = J; K < I; ++K) {
+                const int K0 = WG_TB * K;
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    const int kr = K0 + 4 * s + g;
+                    tt = WG_MFMA(wg_el(Sm, ld, ma, kr, I0 + r16),              // L[I0+r][kr] (upper)
+                                 wg_el(Sm, ld, ma, kr, J0 + r16, K == J), tt);   // X[kr][J0+j]
+                }
+            }
+            wg_d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+                acc = WG_MFMA(-wg_el(Sm, ld, ma, I0 + r16, I0 + 4 * s + g, true), tt[s], acc);   // -X_II T
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int ri = I0 + g + 4 * q, cj = J0 + r16;
+                if (ri < ma && cj < ma) Sm[ri * ld + cj] = acc[q];
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// M^-1 = X^T X over the whole ma x ma (both triangles), from wg_blk_trtri's X
+PHX_HD void wg_blk_lauum(double* Sm, int ld, int ma) {
+    const int nb = (ma + WG_TB - 1) / WG_TB;
+    const int l = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6), r16 = l & 15, g = l >> 4;
+    const int ntile = nb * (nb + 1) / 2;
+    constexpr int TPW = (WG_BLK_MAX / WG_TB) * (WG_BLK_MAX / WG_TB + 1) / 2 / (WG_NT / 64) + 1;
+    wg_d4 acc[TPW];
+    int tI[TPW], tJ[TPW];
+#pragma unroll
+    for (int u = 0; u < TPW; ++u) {
+        const int t = wv + u * (WG_NT / 64);
+        tI[u] = -1;
+        tJ[u] = 0;
+        acc[u] = wg_d4{0.0, 0.0, 0.0, 0.0};
+        if (t >= ntile) continue;
+        int I = 0;
+        while ((I + 1) * (I + 2) / 2 <= t) ++I;
+        const int J = t - I * (I + 1) / 2;
+        tI[u] = I;
+        tJ[u] = J;
+        for (int K = I; K < nb; ++K) {
+            const int K0 = WG_TB * K;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int kr = K0 + 4 * s + g;
+                acc[u] = WG_MFMA(wg_el(Sm, ld, ma, kr, WG_TB * I + r16, true),    // X[kr][I0+r]
+                                 wg_el(Sm, ld, ma, kr, WG_TB * J + r16, true), acc[u]);
+            }
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < TPW; ++u) {
+        if (tI[u] < 0) continue;
+        const int I0 = WG_TB * tI[u], J0 = WG_TB * tJ[u];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int ri = I0 + g + 4 * q, cj = J0 + r16;
+            if (ri < ma && cj < ma) {
+                Sm[ri * ld + cj] = acc[u][q];
+                Sm[cj * ld + ri] = acc[u][q];
+            }
+        }
+    }
+    __syncthreads();
+}
+#else
+// Host (tests/emu, WG_NT = 1): the scalar steps in the same storage
+PHX_HD bool wg_blk_cholesky(double* Sm, int ld, int ma, double* dg, int32_t* flag) {
+    (void)flag;
+    for (int j = 0; j < ma; ++j) {
+        const double d = Sm[j * ld + j];
+        if (!(d > 0.0)) return false;
+        const double sd = sqrt(d);
+        dg[j] = 1.0 / sd;
+        for (int i = j + 1; i < ma; ++i) Sm[j * ld + i] = Sm[i * ld + j] / sd;
+        for (int i = j + 1; i < ma; ++i)
+            for (int k = j + 1; k <= i; ++k) Sm[i * ld + k] = fma(-Sm[j * ld + i], Sm[j * ld + k], Sm[i * ld + k]);
+    }
+    return true;
+}
+PHX_HD void wg_blk_trtri(double* Sm, int ld, int ma, const double* dg) {
+    for (int c = 0; c < ma; ++c) {
+        Sm[c * ld + c] = dg[c];
+        for (int i = c + 1; i < ma; ++i) {
+            double v = 0.0;
+            for (int k = c; k < i; ++k) v = fma(Sm[k * ld + i], Sm[k * ld + c], v);
+            Sm[i * ld + c] = -v * dg[i];
+        }
+    }
+}
+PHX_HD void wg_blk_lauum(double* Sm, int ld, int ma) {
+    // row by row from the bottom: M[i][j] (j <= i) needs X rows >= i only,
+    // and row i of X is no longer needed once M's row i is written
+    for (int i = 0; i < ma; ++i)
+        for (int j = 0; j <= i; ++j) {
+            double v = 0.0;
+            for (int k = i; k < ma; ++k) v = fma(Sm[k * ld + i], Sm[k * ld + j], v);
+            Sm[j * ld + i] = v;            // the upper part first (X lives in the lower)
+        }
+    for (int i = 0; i < ma; ++i)
+        for (int j = 0; j < i; ++j) Sm[i * ld + j] = Sm[j * ld + i];
+}
+#endif
+
 // Returns (uniformly) the number of rounds the lane used when the point in
 // L.xp / L.z passes the KKT certificate, else 0; rounds > 1 allow primal-dual
 // active-set updates in between.
+// BLK (Schur complements of at most WG_BLK_MAX rows): the blocked MFMA
+// factor, inverse and M^-1 = X^T X (wg_blk_*) and one dense mat-vec per
+// refinement step; else the scalar paired-pivot Cholesky, the explicit inverse
+// of its factor and two triangular mat-vecs per step.
+template <bool BLK>
 PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts& O, int s, const WgLds& L,
                    int rounds, double tol0, unsigned long long* prof = nullptr) {
     WG_T0();
@@ -319,7 +606,7 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
                 const double* f = G.fac + (int64_t)s * G.fac_stride;
                 for (int e = WG_TID; e < ma * ld; e += WG_NT) {
                     const int i = e / ld, c = e - i * ld;
-                    if (c <= i) L.Sm[e] = f[e];
+                    if (BLK ? c < ma : c <= i) L.Sm[e] = f[e];
                 }
                 WG_SYNC();
                 WG_CNT(10);
@@ -348,6 +635,13 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
             }
             WG_SYNC();
             WG_TP(1);
+          if (BLK) {
+            if (!wg_blk_cholesky(L.Sm, ld, ma, L.dg, L.flag + 2)) return 0;
+            WG_TP(2);
+            wg_blk_trtri(L.Sm, ld, ma, L.dg);
+            wg_blk_lauum(L.Sm, ld, ma);
+            WG_TP(3);
+          } else {
             // ---- Cholesky: trailing update on the lower part, L[i][k] (i > k)
             //      stored transposed at Sm[k*ld+i], 1/diagonal in dg ----
             // (a quad per row: its four threads take interleaved columns k, so
@@ -438,6 +732,7 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
             }
             WG_SYNC();
             WG_TP(3);
+          }
         }
         // ---- iterative refinement on the unregularised KKT (a proximal-point
         //      iteration) ----
@@ -461,6 +756,22 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
                 L.t[q] = adr - (b - ax);
             }
             WG_SYNC();
+            if (BLK) {
+                // dz = M^-1 t (full rows; compact order) into u
+                for (int i = WG_QID; i < ma; i += WG_QN) {
+                    double v0 = 0.0, v1 = 0.0;
+                    const double* row = L.Sm + (size_t)i * ld;
+                    int k = WG_QL;
+                    for (; k + WG_QW < ma; k += 2 * WG_QW) {
+                        v0 += row[k] * L.t[k];
+                        v1 += row[k + WG_QW] * L.t[k + WG_QW];
+                    }
+                    for (; k < ma; k += WG_QW) v0 += row[k] * L.t[k];
+                    const double v = wg_quad_sum(v0 + v1);
+                    if (WG_QL == 0) L.u[i] = v;
+                }
+                WG_SYNC();
+            } else {
             // u = L^-1 t ; then t = L^-T u (dz, compact order)
             for (int i = WG_QID; i < ma; i += WG_QN) {
                 double v0 = 0.0, v1 = 0.0;
@@ -487,13 +798,15 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
                 if (WG_QL == 0) L.t[k] = v;
             }
             WG_SYNC();
+            }
+            const double* dz = BLK ? L.u : L.t;
             double dmax = 0.0, xmax = 0.0;
             for (int j = WG_TID; j < n; j += WG_NT) {
                 if (L.cc[j]) continue;
                 double atz = 0.0;
                 for (int k = cp[j]; k < cp[j + 1]; ++k) {
                     const int q = L.pos[ri[k]];
-                    if (q >= 0) atz += L.a[c2[k]] * L.t[q];
+                    if (q >= 0) atz += L.a[c2[k]] * dz[q];
                 }
                 const double dx = (L.r1[j] - atz) / (L.pp[j] + reg);
                 const double x = L.xp[j] + dx;
@@ -503,8 +816,8 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
             }
             for (int q = WG_TID; q < ma; q += WG_NT) {
                 const int i = L.ar[q];
-                const double zn = L.z[i] + L.t[q];
-                dmax = fmax(dmax, fabs(L.t[q]));
+                const double zn = L.z[i] + dz[q];
+                dmax = fmax(dmax, fabs(dz[q]));
                 xmax = fmax(xmax, fabs(zn));
                 L.z[i] = zn;
             }
@@ -547,6 +860,12 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
             if (!(ax - ax == 0.0) || !(L.z[i] - L.z[i] == 0.0)) bad = true;
             if (ax < bl && (bl - ax) / dr > ptol * (1.0 + fabs(bl / dr))) bad = true;
             if (ax > bu && (ax - bu) / dr > ptol * (1.0 + fabs(bu / dr))) bad = true;
+            // complementarity: an active row sits at its side (the refinement's
+            // fixed point; a solve whose refinement stopped short fails here)
+            if (L.rc[i]) {
+                const double b = L.rc[i] == 1 ? bl : bu;
+                if (fabs(ax - b) / dr > ptol * (1.0 + fabs(b / dr))) bad = true;
+            }
             if (L.rc[i] && !(bl == bu)) {
                 const double y = -L.z[i] * dr;
                 if (L.rc[i] == 1 && y < -dtol) bad = true;
@@ -565,7 +884,7 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
                 double* f = G.fac + (int64_t)s * G.fac_stride;
                 for (int e = WG_TID; e < ma * ld; e += WG_NT) {
                     const int i = e / ld, c = e - i * ld;
-                    if (c <= i) f[e] = L.Sm[e];
+                    if (BLK ? c < ma : c <= i) f[e] = L.Sm[e];
                 }
                 int8_t* kc = G.key + (int64_t)s * G.key_stride;
                 double* pk = G.pkey + (int64_t)s * (G.N + 1);

@@ -39,6 +39,11 @@ case "$1" in
   s10) # the 1M configuration's loop (r04 s5: 10.9 ms per iteration, unfused)
        PHX_ITERK_DEBUG=1 $J "bench:r04_s10_1m:--only C3x1M --no-cpu-baseline --no-conv --steps 10 --warmup 1" && \
        PHX_QUERY_MS=0 $J "bench:r04_s10_1m_q0:--only C3x1M --no-cpu-baseline --no-conv --steps 10 --warmup 1" ;;
+  s11) # the blocked MFMA Schur inverse in the workgroup solver: tests, C2 / C5a with and without, phase clocks
+       $J "test:tests/test_wg_blk.py tests/test_sslp.py tests/test_bundles.py tests/test_trajectories.py tests/test_gpu_parity.py -k 'blocked or sslp or bundles or cm10 or wg or trajector'" \
+          "bench:r04_s11_c2:--only C2 $A" "bench:r04_s11_c5a:--only C5a $A" && \
+       PHX_WG_PROF=1 $J "bench:r04_s11_c2_wgprof:--only C2 $A" "bench:r04_s11_c5a_wgprof:--only C5a $A" && \
+       PHX_WG_BLK=0 $J "bench:r04_s11_c2_scalar:--only C2 $A" "bench:r04_s11_c5a_scalar:--only C5a $A" ;;
   pmc) # PMC passes on the final kernels (one counter group per pass): FETCH_SIZE, WRITE_SIZE per config,
        # the SQ instruction / wait counters for the headline and the per-rank slice
        $J "pmc:r04_pmc_c3_fetch:FETCH_SIZE:$B" "pmc:r04_pmc_c3_write:WRITE_SIZE:$B" "pmc:r04_pmc_c3_sq:$SQ:$B" \
