@@ -40,7 +40,7 @@ case "$1" in
        PHX_ITERK_DEBUG=1 $J "bench:r04_s10_1m:--only C3x1M --no-cpu-baseline --no-conv --steps 10 --warmup 1" && \
        PHX_QUERY_MS=0 $J "bench:r04_s10_1m_q0:--only C3x1M --no-cpu-baseline --no-conv --steps 10 --warmup 1" ;;
   s11) # the blocked MFMA Schur inverse in the workgroup solver: tests, C2 / C5a with and without, phase clocks
-       $J "test:tests/test_wg_blk.py tests/test_sslp.py tests/test_bundles.py tests/test_trajectories.py tests/test_gpu_parity.py -k 'blocked or sslp or bundles or cm10 or wg or trajector'" \
+       $J "test:tests/test_wg_blk.py tests/test_sslp.py tests/test_bundles.py tests/test_trajectories.py" \
           "bench:r04_s11_c2:--only C2 $A" "bench:r04_s11_c5a:--only C5a $A" && \
        PHX_WG_PROF=1 $J "bench:r04_s11_c2_wgprof:--only C2 $A" "bench:r04_s11_c5a_wgprof:--only C5a $A" && \
        PHX_WG_BLK=0 $J "bench:r04_s11_c2_scalar:--only C2 $A" "bench:r04_s11_c5a_scalar:--only C5a $A" ;;
