@@ -523,11 +523,14 @@ PHX_HD void wg_blk_lauum(double* Sm, int ld, int ma) {
 // Returns (uniformly) the number of rounds the lane used when the point in
 // L.xp / L.z passes the KKT certificate, else 0; rounds > 1 allow primal-dual
 // active-set updates in between.
-// BLK (Schur complements of at most WG_BLK_MAX rows): the blocked MFMA
-// factor, inverse and M^-1 = X^T X (wg_blk_*) and one dense mat-vec per
-// refinement step; else the scalar paired-pivot Cholesky, the explicit inverse
-// of its factor and two triangular mat-vecs per step.
-template <bool BLK>
+// BLK (Schur complements of at most WG_BLK_MAX rows): 1, the blocked MFMA
+// factor and inverse (wg_blk_cholesky, wg_blk_trtri) in the scalar path's
+// storage; 2, also M^-1 = X^T X (wg_blk_lauum) and one dense mat-vec per
+// refinement step (measured: as many flops, but 16 % more active-set rounds on
+// farmer cm=10 -- the emulation shows the same -- so not the default); 0, the
+// scalar paired-pivot Cholesky and explicit inverse.  1 and 0 refine with two
+// triangular mat-vecs per step.
+template <int BLK>
 PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts& O, int s, const WgLds& L,
                    int rounds, double tol0, unsigned long long* prof = nullptr) {
     WG_T0();
@@ -606,7 +609,7 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
                 const double* f = G.fac + (int64_t)s * G.fac_stride;
                 for (int e = WG_TID; e < ma * ld; e += WG_NT) {
                     const int i = e / ld, c = e - i * ld;
-                    if (BLK ? c < ma : c <= i) L.Sm[e] = f[e];
+                    if (BLK == 2 ? c < ma : c <= i) L.Sm[e] = f[e];
                 }
                 WG_SYNC();
                 WG_CNT(10);
@@ -639,7 +642,7 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
             if (!wg_blk_cholesky(L.Sm, ld, ma, L.dg, L.flag + 2)) return 0;
             WG_TP(2);
             wg_blk_trtri(L.Sm, ld, ma, L.dg);
-            wg_blk_lauum(L.Sm, ld, ma);
+            if (BLK == 2) wg_blk_lauum(L.Sm, ld, ma);
             WG_TP(3);
           } else {
             // ---- Cholesky: trailing update on the lower part, L[i][k] (i > k)
@@ -756,7 +759,7 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
                 L.t[q] = adr - (b - ax);
             }
             WG_SYNC();
-            if (BLK) {
+            if (BLK == 2) {
                 // dz = M^-1 t (full rows; compact order) into u
                 for (int i = WG_QID; i < ma; i += WG_QN) {
                     double v0 = 0.0, v1 = 0.0;
@@ -799,7 +802,7 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
             }
             WG_SYNC();
             }
-            const double* dz = BLK ? L.u : L.t;
+            const double* dz = BLK == 2 ? L.u : L.t;
             double dmax = 0.0, xmax = 0.0;
             for (int j = WG_TID; j < n; j += WG_NT) {
                 if (L.cc[j]) continue;
@@ -862,10 +865,12 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
             if (ax > bu && (ax - bu) / dr > ptol * (1.0 + fabs(bu / dr))) bad = true;
             // complementarity: an active row sits at its side (the refinement's
             // fixed point; a solve whose refinement stopped short fails here)
+#ifndef PHX_WG_NO_COMPL
             if (L.rc[i]) {
                 const double b = L.rc[i] == 1 ? bl : bu;
                 if (fabs(ax - b) / dr > ptol * (1.0 + fabs(b / dr))) bad = true;
             }
+#endif
             if (L.rc[i] && !(bl == bu)) {
                 const double y = -L.z[i] * dr;
                 if (L.rc[i] == 1 && y < -dtol) bad = true;
@@ -884,7 +889,7 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
                 double* f = G.fac + (int64_t)s * G.fac_stride;
                 for (int e = WG_TID; e < ma * ld; e += WG_NT) {
                     const int i = e / ld, c = e - i * ld;
-                    if (BLK ? c < ma : c <= i) f[e] = L.Sm[e];
+                    if (BLK == 2 ? c < ma : c <= i) f[e] = L.Sm[e];
                 }
                 int8_t* kc = G.key + (int64_t)s * G.key_stride;
                 double* pk = G.pkey + (int64_t)s * (G.N + 1);

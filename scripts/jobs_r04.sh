@@ -44,6 +44,12 @@ case "$1" in
           "bench:r04_s11_c2:--only C2 $A" "bench:r04_s11_c5a:--only C5a $A" && \
        PHX_WG_PROF=1 $J "bench:r04_s11_c2_wgprof:--only C2 $A" "bench:r04_s11_c5a_wgprof:--only C5a $A" && \
        PHX_WG_BLK=0 $J "bench:r04_s11_c2_scalar:--only C2 $A" "bench:r04_s11_c5a_scalar:--only C5a $A" ;;
+  s12) # workgroup solver modes: blocked factor + inverse (default), + X^T X, scalar
+       $J "test:tests/test_wg_blk.py tests/test_sslp.py tests/test_bundles.py tests/test_trajectories.py" \
+          "bench:r04_s12_c2:--only C2 $A" "bench:r04_s12_c5a:--only C5a $A" && \
+       PHX_WG_PROF=1 $J "bench:r04_s12_c2_wgprof:--only C2 $A" "bench:r04_s12_c5a_wgprof:--only C5a $A" && \
+       PHX_WG_BLK=2 $J "bench:r04_s12_c2_blk2:--only C2 $A" "bench:r04_s12_c5a_blk2:--only C5a $A" && \
+       PHX_WG_BLK=0 $J "bench:r04_s12_c2_scalar:--only C2 $A" "bench:r04_s12_c5a_scalar:--only C5a $A" ;;
   pmc) # PMC passes on the final kernels (one counter group per pass): FETCH_SIZE, WRITE_SIZE per config,
        # the SQ instruction / wait counters for the headline and the per-rank slice
        $J "pmc:r04_pmc_c3_fetch:FETCH_SIZE:$B" "pmc:r04_pmc_c3_write:WRITE_SIZE:$B" "pmc:r04_pmc_c3_sq:$SQ:$B" \
