@@ -298,9 +298,12 @@ __device__ bool wg_blk_diag(double* Sm, int ld, int ma, int p0, double* dg) {
         a[q] = in ? v : (r == c ? 1.0 : 0.0);
     }
     bool ok = true;
-#pragma unroll
+#pragma unroll 1
     for (int j = 0; j < WG_TB; ++j) {
-        const double colj = a[j & 3];     // column j's slot, before this step changes it
+        // column j's slot, before this step changes it (a select over the four
+        // slots: j is uniform; the loop stays rolled, for the register budget)
+        const int js = j & 3;
+        const double colj = js == 0 ? a[0] : (js == 1 ? a[1] : (js == 2 ? a[2] : a[3]));
         const double d = wg_readlane64(colj, j + 16 * (j >> 2));    // a_jj
         ok = ok && d > 0.0;
         const double isd = 1.0 / sqrt(d);
@@ -338,17 +341,13 @@ PHX_HD bool wg_blk_cholesky(double* Sm, int ld, int ma, double* dg, int32_t* fla
         if (*flag) return false;
         if (P + 1 == nb) break;
         // rows below: L[i][p0+j] = (W[i][p0+j] - sum_{k<j} L[i][p0+k] L[p0+j][p0+k]) / L_jj
+        // (the solved entries are re-read from LDS, not held in registers: the
+        // kernel stays at four workgroups per CU)
         for (int i = p0 + WG_TB + (int)threadIdx.x; i < ma; i += WG_NT) {
-            double x[WG_TB];
-#pragma unroll
-            for (int j = 0; j < WG_TB; ++j) {
-                if (j < w) {
-                    double v = Sm[i * ld + p0 + j];
-#pragma unroll
-                    for (int k = 0; k < j; ++k) v = fma(-x[k], Sm[(p0 + k) * ld + p0 + j], v);
-                    x[j] = v * dg[p0 + j];
-                    Sm[(p0 + j) * ld + i] = x[j];
-                }
+            for (int j = 0; j < w; ++j) {
+                double v = Sm[i * ld + p0 + j];
+                for (int k = 0; k < j; ++k) v = fma(-Sm[(p0 + k) * ld + i], Sm[(p0 + k) * ld + p0 + j], v);
+                Sm[(p0 + j) * ld + i] = v * dg[p0 + j];
             }
         }
         __syncthreads();
@@ -390,20 +389,11 @@ PHX_HD void wg_blk_trtri(double* Sm, int ld, int ma, const double* dg) {
         const int p0 = (e >> 4) * WG_TB, c = e & 15;
         const int w = ma - p0 < WG_TB ? ma - p0 : WG_TB;
         if (c >= w) continue;
-        double x[WG_TB];
-#pragma unroll
-        for (int i = 0; i < WG_TB; ++i) {
-            if (i < c || i >= w) continue;
-            if (i == c) {
-                x[i] = dg[p0 + c];
-            } else {
-                double v = 0.0;
-#pragma unroll
-                for (int k = 0; k < i; ++k)
-                    if (k >= c) v = fma(Sm[(p0 + k) * ld + p0 + i], x[k], v);
-                x[i] = -v * dg[p0 + i];
-            }
-            Sm[(p0 + i) * ld + p0 + c] = x[i];
+        Sm[(p0 + c) * ld + p0 + c] = dg[p0 + c];
+        for (int i = c + 1; i < w; ++i) {
+            double v = 0.0;
+            for (int k = c; k < i; ++k) v = fma(Sm[(p0 + k) * ld + p0 + i], Sm[(p0 + k) * ld + p0 + c], v);
+            Sm[(p0 + i) * ld + p0 + c] = -v * dg[p0 + i];
         }
     }
     __syncthreads();
