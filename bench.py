@@ -507,6 +507,8 @@ def run_config(name, w, args, K, so, world, dev):
                                 *pmc_traffic(kernel, CONFIG_PMC_TAG.get(name, name))),
            "solver": ph._native.jit_info(ph._ctx).decode(), "not_optimal": nbad, "setup_s": setup,
            "loop": "phx_iterk (device-driven)" if st is not None else "PHBase host loop (deferred solves)",
+           "iterk": ({k: st.get(k) for k in ("iters", "fused", "straggler_stops", "stragglers", "warm_launches")}
+                     if st is not None else None),
            "solver_options": w.get("so", {})}
     if w.get("cpu") and not args.no_cpu_baseline:
         c = w["cpu"]
@@ -606,6 +608,8 @@ def main():
         "loop": ("PHBase.iterk_loop -> phx_iterk (device-driven, depth %d%s)"
                  % (args.depth, ", fused" if st and st.get("fused") else "")) if st else "PHBase host loop",
         "not_optimal": nbad, "setup_s": t_setup, "warmup_s": t_warm,
+        "iterk": ({k: st.get(k) for k in ("iters", "fused", "straggler_stops", "stragglers", "warm_launches")}
+                  if st else None),
         "solver": ph._native.jit_info(ph._ctx).decode(),
         "final": final_state(ph),
     }

@@ -50,6 +50,9 @@ case "$1" in
        PHX_WG_PROF=1 $J "bench:r04_s12_c2_wgprof:--only C2 $A" "bench:r04_s12_c5a_wgprof:--only C5a $A" && \
        PHX_WG_BLK=2 $J "bench:r04_s12_c2_blk2:--only C2 $A" "bench:r04_s12_c5a_blk2:--only C5a $A" && \
        PHX_WG_BLK=0 $J "bench:r04_s12_c2_scalar:--only C2 $A" "bench:r04_s12_c5a_scalar:--only C5a $A" ;;
+  s13) # the 1M loop's straggler stops: fused kernel vs the legacy fused launch
+       $J "bench:r04_s13_1m:--only C3x1M --no-cpu-baseline --no-conv --steps 10 --warmup 1" && \
+       PHX_FZ_LEGACY=1 $J "bench:r04_s13_1m_legacy:--only C3x1M --no-cpu-baseline --no-conv --steps 10 --warmup 1" ;;
   pmc) # PMC passes on the final kernels (one counter group per pass): FETCH_SIZE, WRITE_SIZE per config,
        # the SQ instruction / wait counters for the headline and the per-rank slice
        $J "pmc:r04_pmc_c3_fetch:FETCH_SIZE:$B" "pmc:r04_pmc_c3_write:WRITE_SIZE:$B" "pmc:r04_pmc_c3_sq:$SQ:$B" \
