@@ -553,10 +553,10 @@ PHX_LD void ipm_opaque(double* x, double* zl, double* zu, double* rl, double* ru
 #define PHX_IPM_WS_ PT::ipm_ws()
 #endif
 template <class PT>
-PHX_LD double ipm_core(const Data<PT>& D, int max_it, double tol, double* x, double* y, int* its) {
+PHX_LD double ipm_core(const Data<PT>& D, int max_it, double tol, double* x, double* y, int* its,
+                       double xs = PHX_IPM_XS_, double zs = PHX_IPM_ZS_, double ws = PHX_IPM_WS_) {
     constexpr int NN = PT::NMAX_N, MM = PT::NMAX_M, TT = PT::NMAX_M * (PT::NMAX_M + 1) / 2;
     const double reg = 1e-10;
-    const double xs = PHX_IPM_XS_, zs = PHX_IPM_ZS_, ws = PHX_IPM_WS_;
     double zl[NN], zu[NN], s[MM], wl[MM], wu[MM];
     // start point (cost-aware multipliers)
     PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
@@ -1568,7 +1568,17 @@ PHX_LD void ipm_lane(const LaneIO& io, int sc) {
     const int64_t S = io.S;
     double x[NN], y[MM];
     int its = 0;
-    const double err = ipm_core<PT>(D, io.max_it, io.ipm_tol, x, y, &its);
+    // the problem-scaled start first; a lane whose interior point fails from it
+    // runs again from the unit start (farmer 1M, emulation: 1 of 10^6 lanes
+    // broke down from the scaled start and converged from the unit one; the
+    // generic path it was left to took 100 ms for it).  (A loop, so the
+    // interior point is inlined once.)
+    double err = 1e300;
+    for (int attempt = 0; attempt < 2 && !(err < 1e-4); ++attempt) {
+        const bool unit = attempt > 0;
+        err = ipm_core<PT>(D, io.max_it, io.ipm_tol, x, y, &its, unit ? 1.0 : PHX_IPM_XS_, unit ? 1.0 : PHX_IPM_ZS_,
+                           unit ? 1.0 : PHX_IPM_WS_);
+    }
     PHX_UNROLL for (int j = 0; j < PT::n(); ++j) io.ipm_x[j * S + sc] = x[j];
     PHX_UNROLL for (int i = 0; i < PT::m(); ++i) io.ipm_y[i * S + sc] = y[i];
     io.err[sc] = err;
@@ -1644,6 +1654,7 @@ PHX_LD bool all_lane(const LaneIO& io, int sc, int rescue) {
     }
     LaneIO io3 = io;
     io3.single_after = 1;          // (the cold pass after warm passes: single changes, phx_kernels.hip)
+    if (rescue > io3.as_rounds) io3.as_rounds = rescue;   // as enqueue_lane_solve's cold pass
     ipm_lane<PT>(io3, sc);
     return cold_rounds_lane<PT>(io3, sc);
 }
