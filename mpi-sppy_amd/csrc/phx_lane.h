@@ -1595,11 +1595,17 @@ PHX_LD bool cold_rounds_lane(const LaneIO& io, int sc) {
     PHX_UNROLL for (int i = 0; i < PT::m(); ++i) y[i] = io.ipm_y[(int64_t)i * S + sc];
     const double err = io.err[sc];
     const int its = io.iters[sc];
-    if (err < 1e-4) {
+    // classification tolerances: the interior point's own accuracy, then (a
+    // lane whose rounds cycle from that set: degenerate faces) looser ones
+#ifndef PHX_COLD_TRIES
+#define PHX_COLD_TRIES 3
+#endif
+    for (int attempt = 0; attempt < PHX_COLD_TRIES && err < 1e-4; ++attempt) {
+        const double tol = attempt == 0 ? fmin(1e-4, fmax(1e-9, 10.0 * err)) : (attempt == 1 ? 1e-6 : 1e-4);
         ASet<PT> a;
         {
             const Data<PT> D(io, sc);
-            classify<PT>(D, x, y, fmin(1e-4, fmax(1e-9, 10.0 * err)), a);
+            classify<PT>(D, x, y, tol, a);
         }
         double xp[NN], z[MM];
         PHX_UNROLL for (int j = 0; j < PT::n(); ++j) xp[j] = x[j];
