@@ -55,6 +55,9 @@ case "$1" in
        PHX_FZ_LEGACY=1 $J "bench:r04_s13_1m_legacy:--only C3x1M --no-cpu-baseline --no-conv --steps 10 --warmup 1" ;;
   s14) # the 1M loop's kernel trace
        $J "prof:r04_s14_1m_prof:--only C3x1M --no-cpu-baseline --no-conv --steps 10 --warmup 1" ;;
+  s15) # the 1M configuration after the cold-path fixes; the per-rank slice's profile
+       $J "bench:r04_s15_1m:--only C3x1M --no-cpu-baseline --no-conv --steps 10 --warmup 1" \
+          "bench:r04_s15_c3s8:$S8" "prof:r04_s15_c3s8_prof:$S8" "bench:r04_s15_bench:$H" ;;
   pmc) # PMC passes on the final kernels (one counter group per pass): FETCH_SIZE, WRITE_SIZE per config,
        # the SQ instruction / wait counters for the headline and the per-rank slice
        $J "pmc:r04_pmc_c3_fetch:FETCH_SIZE:$B" "pmc:r04_pmc_c3_write:WRITE_SIZE:$B" "pmc:r04_pmc_c3_sq:$SQ:$B" \
