@@ -58,13 +58,13 @@ case "$1" in
   s15) # the 1M configuration after the cold-path fixes; the per-rank slice's profile
        $J "bench:r04_s15_1m:--only C3x1M --no-cpu-baseline --no-conv --steps 10 --warmup 1" \
           "bench:r04_s15_c3s8:$S8" "prof:r04_s15_c3s8_prof:$S8" "bench:r04_s15_bench:$H" ;;
-  pmc) # PMC passes on the final kernels (one counter group per pass): FETCH_SIZE, WRITE_SIZE per config,
-       # the SQ instruction / wait counters for the headline and the per-rank slice
+  pmc1) # PMC passes on the final kernels (one counter group per pass): the lane kernels
        $J "pmc:r04_pmc_c3_fetch:FETCH_SIZE:$B" "pmc:r04_pmc_c3_write:WRITE_SIZE:$B" "pmc:r04_pmc_c3_sq:$SQ:$B" \
           "pmc:r04_pmc_s8_fetch:FETCH_SIZE:$S8" "pmc:r04_pmc_s8_write:WRITE_SIZE:$S8" "pmc:r04_pmc_s8_sq:$SQ:$S8" \
           "pmc:r04_pmc_1m_fetch:FETCH_SIZE:$M" "pmc:r04_pmc_1m_write:WRITE_SIZE:$M" \
-          "pmc:r04_pmc_c2_fetch:FETCH_SIZE:--only C2 $A" "pmc:r04_pmc_c2_write:WRITE_SIZE:--only C2 $A" \
-          "pmc:r04_pmc_c4_fetch:FETCH_SIZE:--only C4 $A" "pmc:r04_pmc_c4_write:WRITE_SIZE:--only C4 $A" \
+          "pmc:r04_pmc_c4_fetch:FETCH_SIZE:--only C4 $A" "pmc:r04_pmc_c4_write:WRITE_SIZE:--only C4 $A" ;;
+  pmc2) # ... the workgroup and sparse solvers
+       $J "pmc:r04_pmc_c2_fetch:FETCH_SIZE:--only C2 $A" "pmc:r04_pmc_c2_write:WRITE_SIZE:--only C2 $A" \
           "pmc:r04_pmc_c5a_fetch:FETCH_SIZE:--only C5a $A" "pmc:r04_pmc_c5a_write:WRITE_SIZE:--only C5a $A" \
           "pmc:r04_pmc_c5b_fetch:FETCH_SIZE:--only C5b $A" "pmc:r04_pmc_c5b_write:WRITE_SIZE:--only C5b $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
