@@ -60,6 +60,9 @@ case "$1" in
           "bench:r04_s15_c3s8:$S8" "prof:r04_s15_c3s8_prof:$S8" "bench:r04_s15_bench:$H" ;;
   s16) # the 100k Iter0: unseeded (interior point on every lane) against seeded
        $J "bench:r04_s16_bench:$H" && PHX_NO_SEED=1 $J "bench:r04_s16_bench_noseed:$H" "prof:r04_s16_noseed_prof:$H --ar-probe 0" ;;
+  s17) # the 1M Iter0: unseeded against seeded
+       $J "bench:r04_s17_1m:--only C3x1M --no-cpu-baseline --no-conv --steps 10 --warmup 1" && \
+       PHX_NO_SEED=1 $J "bench:r04_s17_1m_noseed:--only C3x1M --no-cpu-baseline --no-conv --steps 10 --warmup 1" ;;
   pmc1) # PMC passes on the final kernels (one counter group per pass): the lane kernels
        $J "pmc:r04_pmc_c3_fetch:FETCH_SIZE:$B" "pmc:r04_pmc_c3_write:WRITE_SIZE:$B" "pmc:r04_pmc_c3_sq:$SQ:$B" \
           "pmc:r04_pmc_s8_fetch:FETCH_SIZE:$S8" "pmc:r04_pmc_s8_write:WRITE_SIZE:$S8" "pmc:r04_pmc_s8_sq:$SQ:$S8" \
