@@ -63,6 +63,8 @@ case "$1" in
   s17) # the 1M Iter0: unseeded against seeded
        $J "bench:r04_s17_1m:--only C3x1M --no-cpu-baseline --no-conv --steps 10 --warmup 1" && \
        PHX_NO_SEED=1 $J "bench:r04_s17_1m_noseed:--only C3x1M --no-cpu-baseline --no-conv --steps 10 --warmup 1" ;;
+  s18) # the whole GPU suite, then the driver's default command
+       $J "test:tests" && $J "bench:r04_s18_default:" ;;
   pmc1) # PMC passes on the final kernels (one counter group per pass): the lane kernels
        $J "pmc:r04_pmc_c3_fetch:FETCH_SIZE:$B" "pmc:r04_pmc_c3_write:WRITE_SIZE:$B" "pmc:r04_pmc_c3_sq:$SQ:$B" \
           "pmc:r04_pmc_s8_fetch:FETCH_SIZE:$S8" "pmc:r04_pmc_s8_write:WRITE_SIZE:$S8" "pmc:r04_pmc_s8_sq:$SQ:$S8" \
