@@ -78,6 +78,7 @@ struct WgPairs {
     int32_t N;
     char* split;          // [S][split_stride] wg_carve's split arrays, or null (all in LDS)
     int64_t split_stride;
+    int32_t single_after = WG_SINGLE_AFTER;   // rounds of full primal-dual changes before single ones
 };
 
 // Carve of the dynamic LDS of one scenario.
@@ -941,7 +942,7 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
         //      the largest wrong-signed multiplier) -- measured on sslp
         //      (emulation, 300 scenarios x 6 iterations): 87 of 1,800 solves
         //      ran out of their 16 full-change rounds, cycling ----
-        const bool single = round + 1 >= WG_SINGLE_AFTER;
+        const bool single = round + 1 >= G.single_after;
         double bk = 0.0;     // the best change's key (0: none): primal 2 + v/(1+v), dual 1 + v/(1+v)
         int bi = -1;         // its element: column j, or n + row i
         for (int j = WG_TID; j < n; j += WG_NT) {

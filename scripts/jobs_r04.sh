@@ -65,8 +65,9 @@ case "$1" in
        PHX_NO_SEED=1 $J "bench:r04_s17_1m_noseed:--only C3x1M --no-cpu-baseline --no-conv --steps 10 --warmup 1" ;;
   s18) # the whole GPU suite, then the driver's default command
        $J "test:tests" && $J "bench:r04_s18_default:" ;;
-  s19) # the workgroup solver's pipeline stops (C5a, C2 traces) with single changes after two rounds
-       $J "prof:r04_s19_c5a_prof:--only C5a $A" "prof:r04_s19_c2_prof:--only C2 $A" "bench:r04_s19_c5a:--only C5a $A" "bench:r04_s19_c2:--only C2 $A" ;;
+  s19) # the workgroup solver's pipeline stops (C5a, C2 traces) with single changes after two rounds, and without
+       $J "prof:r04_s19_c5a_prof:--only C5a $A" "bench:r04_s19_c5a:--only C5a $A" "bench:r04_s19_c2:--only C2 $A" && \
+       PHX_WG_SINGLE_AFTER=99 $J "bench:r04_s19_c5a_full:--only C5a $A" "bench:r04_s19_c2_full:--only C2 $A" ;;
   pmc1) # PMC passes on the final kernels (one counter group per pass): the lane kernels
        $J "pmc:r04_pmc_c3_fetch:FETCH_SIZE:$B" "pmc:r04_pmc_c3_write:WRITE_SIZE:$B" "pmc:r04_pmc_c3_sq:$SQ:$B" \
           "pmc:r04_pmc_s8_fetch:FETCH_SIZE:$S8" "pmc:r04_pmc_s8_write:WRITE_SIZE:$S8" "pmc:r04_pmc_s8_sq:$SQ:$S8" \
