@@ -50,7 +50,7 @@ namespace phx {
 #define WG_QL (WG_NT >= 4 ? (WG_TID & 3) : 0)         // its place in the quad
 #define WG_QW (WG_NT >= 4 ? 4 : 1)                    // threads per quad
 #ifndef WG_SINGLE_AFTER
-#define WG_SINGLE_AFTER 2    // full primal-dual changes in the first rounds, then the worst one only
+#define WG_SINGLE_AFTER 99   // rounds of full primal-dual changes before single ones (PHX_WG_SINGLE_AFTER; 2 measured: sslp -2 %, farmer cm=10 +27 %, r04 s19)
 #endif
 
 // Schur-complement entries (ia >= ib) whose rows share a column, with the CSR
