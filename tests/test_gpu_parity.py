@@ -503,3 +503,13 @@ def test_window_timing_fused_loop_gpu(gpu_lib):
     assert st["fused"] and st["iters"] == K
     assert st["warm_launches"] == K - 1 and st["lane_warm_ms"] > 0.0
     assert np.array_equal(a.W_array(), b.W_array())
+
+
+def test_per_rank_slice_12500_gpu(gpu_lib):
+    """The 8-GPU per-rank slice (C3s8: farmer 12,500 on one GPU): the unseeded
+    Iter0 at one wavefront per SIMD, the one-launch small-batch solve
+    (phx_lane_all) of the first iteration and the one-wave fused kernel
+    (phx_lane_warm_fz1) after it == the Python loop (x-bar, W, nonants,
+    conv, E[obj] to 1e-9; the fused sums run in another fixed order)."""
+    from test_engine_emu import check_native_vs_host
+    check_native_vs_host(gpu_lib, None, "farmer", S=12500, fused=1)
