@@ -1,0 +1,29 @@
+#!/bin/bash
+# Copy the round-4 evidence judged from gpurun_out/ (scratch) into profiles/:
+# PMC summaries (scripts/pmc_summary.py, timed-window launches), rocprofv3
+# kernel statistics of the final traces, the default bench line.
+set -e
+G=gpurun_out
+P=profiles
+S="python3 scripts/pmc_summary.py"
+$S phx_lane_warm_fz --last 49 $G/r04_pmc_c3_fetch $G/r04_pmc_c3_write > $P/r04_pmc_farmer100k_phx_lane_warm_fz.json
+$S phx_lane_warm_fz --last 49 $G/r04_pmc_c3_sq > $P/r04_pmcsq_farmer100k_phx_lane_warm_fz.json
+$S phx_lane_warm_fz1 --last 19 $G/r04_pmc_s8_fetch $G/r04_pmc_s8_write > $P/r04_pmc_farmer12k5_phx_lane_warm_fz1.json
+$S phx_lane_warm_fz1 --last 19 $G/r04_pmc_s8_sq > $P/r04_pmcsq_farmer12k5_phx_lane_warm_fz1.json
+$S phx_lane_warm_fz --last 19 $G/r04_pmc_1m_fetch $G/r04_pmc_1m_write > $P/r04_pmc_farmer1m_phx_lane_warm_fz.json
+$S phx_lane_all --last 10 $G/r04_pmc_c4_fetch $G/r04_pmc_c4_write > $P/r04_pmc_aircond1k_phx_lane_all.json
+$S k_wg_warm --last 10 --skip-idle $G/r04_pmc_c2_fetch $G/r04_pmc_c2_write > $P/r04_pmc_farmercm10_1k_k_wg_warm.json
+$S k_wg_warm --last 10 --skip-idle $G/r04_pmc_c5a_fetch $G/r04_pmc_c5a_write > $P/r04_pmc_sslp10k_k_wg_warm.json
+$S k_sp_solve --last 10 --skip-idle $G/r04_pmc_c5b_fetch $G/r04_pmc_c5b_write > $P/r04_pmc_netdes10k_k_sp_solve.json
+for t in prof c3s8_prof 1m_prof c2_prof c4_prof c5a_prof c5b_prof; do
+  cp $G/r04_final_$t/run_kernel_stats.csv $P/r04_final_${t%_prof}_kernel_stats.csv
+done
+mv $P/r04_final_prof_kernel_stats.csv $P/r04_final_headline_kernel_stats.csv 2>/dev/null || true
+python3 - <<'PY'
+import json
+d = None
+for line in open("gpurun_out/r04_final_default.log"):
+    if line.startswith("{"):
+        d = json.loads(line)
+json.dump(d, open("profiles/r04_final_bench_default.json", "w"), indent=1)
+PY
