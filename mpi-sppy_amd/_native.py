@@ -10,7 +10,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libphx.so")
+# (PHX_LIB_PATH: an experiment's variant build; the product is the in-tree libphx.so)
+LIB_PATH = os.environ.get("PHX_LIB_PATH") or os.path.join(_HERE, "libphx.so")
 
 c_int32 = ctypes.c_int32
 c_double = ctypes.c_double

@@ -191,8 +191,18 @@ PHX_HD void sp_reduce(double* v, double* red, int op) {
 // which zeroes that component of the solve — cholesky_ipm's safeguard
 // (phx_lane.h).
 // ---------------------------------------------------------------------------
+PHX_HD bool sp_factor_once(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds& L, int s, bool ipm_safe);
+// (PHX_SP_FACTOR_TWICE, an experiment build: every factorization done twice,
+// its time measured as the difference)
 PHX_HD bool sp_factor(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds& L, int s,
                       bool ipm_safe = false) {
+#ifdef PHX_SP_FACTOR_TWICE
+    (void)sp_factor_once(P, Y, G, L, s, ipm_safe);
+#endif
+    return sp_factor_once(P, Y, G, L, s, ipm_safe);
+}
+PHX_HD bool sp_factor_once(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds& L, int s,
+                           bool ipm_safe) {
     const int m = P.m, nC = Y.nC, ld = Y.ld;
     // B-row diagonal and the links M_bc
     for (int i = SP_TID; i < m; i += SP_NT) {

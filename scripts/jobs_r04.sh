@@ -68,6 +68,10 @@ case "$1" in
   s19) # the workgroup solver's pipeline stops (C5a, C2 traces) with single changes after two rounds, and without
        $J "prof:r04_s19_c5a_prof:--only C5a $A" "bench:r04_s19_c5a:--only C5a $A" "bench:r04_s19_c2:--only C2 $A" && \
        PHX_WG_SINGLE_AFTER=99 $J "bench:r04_s19_c5a_full:--only C5a $A" "bench:r04_s19_c2_full:--only C2 $A" ;;
+  s20) # the sparse solver's factorization share: every factorization done twice (variant build)
+       $J "bench:r04_s20_c5b:--only C5b $A" "bench:r04_s20_c5a:--only C5a $A" "bench:r04_s20_c2:--only C2 $A" && \
+       PHX_LIB_PATH=$PWD/mpi-sppy_amd/libphx_sptwice.so $J "bench:r04_s20_c5b_twice:--only C5b $A" \
+          "bench:r04_s20_c5a_twice:--only C5a $A" "bench:r04_s20_c2_twice:--only C2 $A" ;;
   final) # the round's evidence: the whole GPU suite, the driver's default command, kernel traces
        $J "test:tests" && $J "bench:r04_final_default:" "prof:r04_final_prof:$H --ar-probe 0" \
           "prof:r04_final_c3s8_prof:$S8" "prof:r04_final_1m_prof:$M" "prof:r04_final_c2_prof:--only C2 $A" \
