@@ -1129,7 +1129,23 @@ template <class PT>
 PHX_LD bool kkt_solve(const Data<PT>& D, const ASet<PT>& a, double* xp, double* z) {
     KFactor<PT> K;
     const AMul<PT> am(a);
+#ifdef PHX_EXP_FACTOR_TWICE
+    // (measurement builds, PHX_LANE_DEFS: the factor's share of a round)
+    (void)kkt_factor<PT>(D, am, K);
+    PHX_UNROLL for (int t = 0; t < PT::NMAX_M * (PT::NMAX_M + 1) / 2; ++t) opaque(K.M[t]);
+#endif
     if (!kkt_factor<PT>(D, am, K)) return false;
+#ifdef PHX_EXP_REFINE_TWICE
+    // (... and the refinement's: run from the same start twice)
+    {
+        double x0[PT::NMAX_N], z0[PT::NMAX_M];
+        PHX_UNROLL for (int j = 0; j < PT::n(); ++j) x0[j] = xp[j];
+        PHX_UNROLL for (int i = 0; i < PT::m(); ++i) z0[i] = z[i];
+        kkt_refine<PT>(D, am, K, RhsFull<PT>{D, a}, xp, z);
+        PHX_UNROLL for (int j = 0; j < PT::n(); ++j) { opaque(xp[j]); xp[j] = x0[j]; }
+        PHX_UNROLL for (int i = 0; i < PT::m(); ++i) { opaque(z[i]); z[i] = z0[i]; }
+    }
+#endif
     kkt_refine<PT>(D, am, K, RhsFull<PT>{D, a}, xp, z);
     return true;
 }

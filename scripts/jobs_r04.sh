@@ -72,6 +72,10 @@ case "$1" in
        $J "bench:r04_s20_c5b:--only C5b $A" "bench:r04_s20_c5a:--only C5a $A" "bench:r04_s20_c2:--only C2 $A" && \
        PHX_LIB_PATH=$PWD/mpi-sppy_amd/libphx_sptwice.so $J "bench:r04_s20_c5b_twice:--only C5b $A" \
           "bench:r04_s20_c5a_twice:--only C5a $A" "bench:r04_s20_c2_twice:--only C2 $A" ;;
+  s21) # the factor's and the refinement's shares of the lane round (JIT measurement defines)
+       $J "bench:r04_s21_c3s8:$S8" "bench:r04_s21_bench:$H" && \
+       PHX_LANE_DEFS=PHX_EXP_FACTOR_TWICE $J "bench:r04_s21_c3s8_f2:$S8" "bench:r04_s21_bench_f2:$H" && \
+       PHX_LANE_DEFS=PHX_EXP_REFINE_TWICE $J "bench:r04_s21_c3s8_r2:$S8" "bench:r04_s21_bench_r2:$H" ;;
   final) # the round's evidence: the whole GPU suite, the driver's default command, kernel traces
        $J "test:tests" && $J "bench:r04_final_default:" "prof:r04_final_prof:$H --ar-probe 0" \
           "prof:r04_final_c3s8_prof:$S8" "prof:r04_final_1m_prof:$M" "prof:r04_final_c2_prof:--only C2 $A" \
