@@ -294,7 +294,11 @@ inline std::string lane_kernel_source(const LaneStructure& L, int warm_waves = 1
     // ... for batches of at most one wavefront per SIMD: the whole register
     // file (VGPRs + AGPRs) for one wave, no scratch spills
     o << "extern \"C\" __global__ void __launch_bounds__(64, 1) phx_lane_warm_fz1(phx_lane::LaneIO io) {\n"
-         "  phx_lane::warm_fused<PT>(io);\n"
+         "#ifdef PHX_FZ1_RELOAD\n"
+         "  phx_lane::warm_fused<PT, false>(io);\n"
+         "#else\n"
+         "  phx_lane::warm_fused<PT, true>(io);\n"
+         "#endif\n"
          "}\n";
     // a whole warm solve (warm rounds, rescue rounds, interior point) in one
     // launch, for batches of at most one wavefront per SIMD (phx_lane.h all_lane)

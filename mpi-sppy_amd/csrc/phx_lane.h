@@ -2054,7 +2054,10 @@ __device__ __forceinline__ void compact_lane(bool still, int sc, int32_t* out, i
 // outputs and x-bar partials come from the certifying round's registers
 // (as_rounds), so the epilogue re-reads nothing.  The same operations as
 // phx_lane_warm's fused path (fz_update_w, warm_lane, fz_epilogue).
-template <class PT>
+// REG (the one-wave-per-SIMD build, 512 registers): every round runs on the
+// data in registers -- the other builds re-load it per round (kept live across
+// the round loop it spilled; a re-load is a memory round trip per round)
+template <class PT, bool REG = false>
 __device__ void warm_fused(const LaneIO& io) {
     const FusedW& f = io.fz;
     constexpr int NS = PT::nslot() > 0 ? PT::nslot() : 1;
@@ -2101,17 +2104,26 @@ __device__ void warm_fused(const LaneIO& io) {
         double xp[PT::NMAX_N], z[PT::NMAX_M];
         PHX_UNROLL for (int j = 0; j < PT::n(); ++j) xp[j] = 0.0;
         PHX_UNROLL for (int i = 0; i < PT::m(); ++i) z[i] = 0.0;
-        // round 0 on the data in registers; later rounds re-load (as_rounds)
+        // round 0 on the data in registers; later rounds re-load (as_rounds),
+        // or with REG stay on them
         int c;
-        {
+        if (REG) {
             const Data<PT> D0(io, sc, av, wv, rv, xb);
             c = io.warm_rounds > 0 ? as_round<PT>(io, D0, a, xp, z, 0) : 2;
+            PHX_NOUNROLL for (int r = 1; r < io.warm_rounds && c == 1; ++r) c = as_round<PT>(io, D0, a, xp, z, r);
+            if (c == 2) PHX_LANE_STAT(3);
             if (c == 0) write_certified<PT>(io, D0, sc, a, xp, z, 0);
-        }
-        if (c == 1 && as_rounds<PT>(io, sc, a, io.warm_rounds, xp, z, 1)) {
-            c = 0;
-            const Data<PT> Dc(io, opaque_index(sc));
-            write_certified<PT>(io, Dc, sc, a, xp, z, 0);
+        } else {
+            {
+                const Data<PT> D0(io, sc, av, wv, rv, xb);
+                c = io.warm_rounds > 0 ? as_round<PT>(io, D0, a, xp, z, 0) : 2;
+                if (c == 0) write_certified<PT>(io, D0, sc, a, xp, z, 0);
+            }
+            if (c == 1 && as_rounds<PT>(io, sc, a, io.warm_rounds, xp, z, 1)) {
+                c = 0;
+                const Data<PT> Dc(io, opaque_index(sc));
+                write_certified<PT>(io, Dc, sc, a, xp, z, 0);
+            }
         }
         if (c != 0) {
             aset_store<PT>(io, sc, a);   // the updated active set seeds the next pass

@@ -76,6 +76,9 @@ case "$1" in
        $J "bench:r04_s21_c3s8:$S8" "bench:r04_s21_bench:$H" && \
        PHX_LANE_DEFS=PHX_EXP_FACTOR_TWICE $J "bench:r04_s21_c3s8_f2:$S8" "bench:r04_s21_bench_f2:$H" && \
        PHX_LANE_DEFS=PHX_EXP_REFINE_TWICE $J "bench:r04_s21_c3s8_r2:$S8" "bench:r04_s21_bench_r2:$H" ;;
+  s22) # the one-wave fused kernel's rounds on register data (no per-round re-load)
+       $J "test:tests/test_gpu_parity.py tests/test_trajectories.py" "bench:r04_s22_c3s8:$S8" "prof:r04_s22_c3s8_prof:$S8" && \
+       PHX_LANE_DEFS=PHX_FZ1_RELOAD $J "bench:r04_s22_c3s8_reload:$S8" ;;
   final) # the round's evidence: the whole GPU suite, the driver's default command, kernel traces
        $J "test:tests" && $J "bench:r04_final_default:" "prof:r04_final_prof:$H --ar-probe 0" \
           "prof:r04_final_c3s8_prof:$S8" "prof:r04_final_1m_prof:$M" "prof:r04_final_c2_prof:--only C2 $A" \
