@@ -79,6 +79,9 @@ case "$1" in
   s22) # the one-wave fused kernel's rounds on register data (no per-round re-load)
        $J "test:tests/test_gpu_parity.py tests/test_trajectories.py" "bench:r04_s22_c3s8:$S8" "prof:r04_s22_c3s8_prof:$S8" && \
        PHX_LANE_DEFS=PHX_FZ1_RELOAD $J "bench:r04_s22_c3s8_reload:$S8" ;;
+  s23) # the one-wave fused kernel at 100k and 1M (waves one after the other on a SIMD)
+       $J "bench:r04_s23_bench:$H" "bench:r04_s23_1m:--only C3x1M --no-cpu-baseline --no-conv --steps 10 --warmup 1" && \
+       PHX_FZ1=1 $J "bench:r04_s23_bench_fz1:$H" "bench:r04_s23_1m_fz1:--only C3x1M --no-cpu-baseline --no-conv --steps 10 --warmup 1" ;;
   final) # the round's evidence: the whole GPU suite, the driver's default command, kernel traces
        $J "test:tests" && $J "bench:r04_final_default:" "prof:r04_final_prof:$H --ar-probe 0" \
           "prof:r04_final_c3s8_prof:$S8" "prof:r04_final_1m_prof:$M" "prof:r04_final_c2_prof:--only C2 $A" \
