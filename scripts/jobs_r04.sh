@@ -82,6 +82,10 @@ case "$1" in
   s23) # the one-wave fused kernel at 100k and 1M (waves one after the other on a SIMD)
        $J "bench:r04_s23_bench:$H" "bench:r04_s23_1m:--only C3x1M --no-cpu-baseline --no-conv --steps 10 --warmup 1" && \
        PHX_FZ1=1 $J "bench:r04_s23_bench_fz1:$H" "bench:r04_s23_1m_fz1:--only C3x1M --no-cpu-baseline --no-conv --steps 10 --warmup 1" ;;
+  s24) # the one-wave fused kernel at 1M: HBM traffic and time again
+       PHX_FZ1=1 $J "pmc:r04_s24_1m_fz1_fetch:FETCH_SIZE:$M" "pmc:r04_s24_1m_fz1_write:WRITE_SIZE:$M" \
+          "bench:r04_s24_1m_fz1:--only C3x1M --no-cpu-baseline --no-conv --steps 10 --warmup 1" && \
+       $J "bench:r04_s24_1m:--only C3x1M --no-cpu-baseline --no-conv --steps 10 --warmup 1" ;;
   final) # the round's evidence: the whole GPU suite, the driver's default command, kernel traces
        $J "test:tests" && $J "bench:r04_final_default:" "prof:r04_final_prof:$H --ar-probe 0" \
           "prof:r04_final_c3s8_prof:$S8" "prof:r04_final_1m_prof:$M" "prof:r04_final_c2_prof:--only C2 $A" \
