@@ -86,6 +86,10 @@ case "$1" in
        PHX_FZ1=1 $J "pmc:r04_s24_1m_fz1_fetch:FETCH_SIZE:$M" "pmc:r04_s24_1m_fz1_write:WRITE_SIZE:$M" \
           "bench:r04_s24_1m_fz1:--only C3x1M --no-cpu-baseline --no-conv --steps 10 --warmup 1" && \
        $J "bench:r04_s24_1m:--only C3x1M --no-cpu-baseline --no-conv --steps 10 --warmup 1" ;;
+  s25) # the one-wave fused kernel at 100k: traffic, and time against the two-wave build twice
+       PHX_FZ1=1 $J "pmc:r04_s25_c3_fz1_fetch:FETCH_SIZE:$B" "pmc:r04_s25_c3_fz1_write:WRITE_SIZE:$B" \
+          "bench:r04_s25_bench_fz1a:$H" && $J "bench:r04_s25_bencha:$H" && PHX_FZ1=1 $J "bench:r04_s25_bench_fz1b:$H" && \
+       $J "bench:r04_s25_benchb:$H" ;;
   final) # the round's evidence: the whole GPU suite, the driver's default command, kernel traces
        $J "test:tests" && $J "bench:r04_final_default:" "prof:r04_final_prof:$H --ar-probe 0" \
           "prof:r04_final_c3s8_prof:$S8" "prof:r04_final_1m_prof:$M" "prof:r04_final_c2_prof:--only C2 $A" \
