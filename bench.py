@@ -428,7 +428,9 @@ def dominant_kernel(ph, K, fused):
             # small-batch solve / the warm pass
             small = -(-b.S // 64) <= simds()
             if st.get("fused"):
-                kname = "phx_lane_warm_fz1" if small else "phx_lane_warm_fz"
+                # (the one-wave build at every size unless PHX_FZ2=1, phx_kernels.hip)
+                fz2 = os.environ.get("PHX_FZ2") == "1"
+                kname = "phx_lane_warm_fz" if (fz2 and not small) else "phx_lane_warm_fz1"
             else:
                 kname = "phx_lane_all" if small else "phx_lane_warm"
             return (kname, st["lane_warm_ms"] / 1e3 / st["warm_launches"], st["warm_launches"],

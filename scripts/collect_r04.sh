@@ -6,11 +6,11 @@ set -e
 G=gpurun_out
 P=profiles
 S="python3 scripts/pmc_summary.py"
-$S phx_lane_warm_fz --last 49 $G/r04_pmc_c3_fetch $G/r04_pmc_c3_write > $P/r04_pmc_farmer100k_phx_lane_warm_fz.json
-$S phx_lane_warm_fz --last 49 $G/r04_pmc_c3_sq > $P/r04_pmcsq_farmer100k_phx_lane_warm_fz.json
+$S phx_lane_warm_fz1 --last 49 $G/r04_pmc_c3_fetch $G/r04_pmc_c3_write > $P/r04_pmc_farmer100k_phx_lane_warm_fz1.json
+$S phx_lane_warm_fz1 --last 49 $G/r04_pmc_c3_sq > $P/r04_pmcsq_farmer100k_phx_lane_warm_fz1.json
 $S phx_lane_warm_fz1 --last 19 $G/r04_pmc_s8_fetch $G/r04_pmc_s8_write > $P/r04_pmc_farmer12k5_phx_lane_warm_fz1.json
 $S phx_lane_warm_fz1 --last 19 $G/r04_pmc_s8_sq > $P/r04_pmcsq_farmer12k5_phx_lane_warm_fz1.json
-$S phx_lane_warm_fz --last 19 $G/r04_pmc_1m_fetch $G/r04_pmc_1m_write > $P/r04_pmc_farmer1m_phx_lane_warm_fz.json
+$S phx_lane_warm_fz1 --last 19 $G/r04_pmc_1m_fetch $G/r04_pmc_1m_write > $P/r04_pmc_farmer1m_phx_lane_warm_fz1.json
 $S phx_lane_all --last 10 $G/r04_pmc_c4_fetch $G/r04_pmc_c4_write > $P/r04_pmc_aircond1k_phx_lane_all.json
 $S k_wg_warm --last 10 --skip-idle $G/r04_pmc_c2_fetch $G/r04_pmc_c2_write > $P/r04_pmc_farmercm10_1k_k_wg_warm.json
 $S k_wg_warm --last 10 --skip-idle $G/r04_pmc_c5a_fetch $G/r04_pmc_c5a_write > $P/r04_pmc_sslp10k_k_wg_warm.json
