@@ -1209,8 +1209,8 @@ PHX_LD bool map_apply(const Data<PT>& D, const LaneIO& io, int sc, double* xp, d
 
 // The largest violation among the flagged changes (kind * 64 + index; kinds:
 // 0/1 column to its lower/upper bound, 2 column freed, 3/4 row to its
-// lower/upper side, 5 row released): the largest relative primal violation,
-// else the largest wrong-signed multiplier.
+// lower/upper side, 5 row released): the larger of the largest relative
+// primal violation and the largest relative wrong-signed multiplier.
 template <class PT, class CM>
 PHX_LD int worst_violation(const Data<PT>& D, CM enter_lo, CM enter_up, CM leave, uint32_t act_lo, uint32_t act_up,
                            uint32_t drop, const double* xp, const double* z, double qmax) {
@@ -1259,15 +1259,28 @@ PHX_LD int worst_violation(const Data<PT>& D, CM enter_lo, CM enter_up, CM leave
         kd = f ? 320 + i : kd;
         bd = f ? v : bd;
     }
+    // the larger of the two (both relative): on aircond's rescue rounds the
+    // slowest lanes need 13-17 single changes instead of 21-26 with the
+    // primal violation always first (emulation, 1,000 scenarios; C4 steady
+    // step 167 -> 148 us, r04_s26); farmer's rounds are the same.
+    // (PHX_SINGLE_PRIMAL_FIRST: the round-3 rule; PHX_SINGLE_DUAL_FIRST: the
+    // multiplier first -- fewer rounds on aircond still, but more cold lanes
+    // after farmer's seeded Iter0.)
+#if defined(PHX_SINGLE_PRIMAL_FIRST)
     return kp >= 0 ? kp : kd;
+#elif defined(PHX_SINGLE_DUAL_FIRST)
+    return kd >= 0 ? kd : kp;
+#else
+    return kp >= 0 && (kd < 0 || bp >= bd) ? kp : kd;
+#endif
 }
 
 // KKT certificate of (xp, z) for active set a (unscaled, relative kkt_tol);
 // on failure applies the primal-dual active-set update (violated bounds/rows
 // enter, wrong-signed multipliers leave).  Returns 0 certified, 1 active set
 // changed, 2 not certified and nothing to change.
-// single: change only the worst violation (the largest relative primal
-// violation, else the largest wrong-signed multiplier) -- the anti-cycling
+// single: change only the worst violation (worst_violation: the largest
+// relative primal violation or wrong-signed multiplier) -- the anti-cycling
 // fallback of the later rounds: the full primal-dual update can cycle on
 // degenerate LP faces, one change at a time walks them like a pivot.
 template <class PT>

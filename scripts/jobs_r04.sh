@@ -90,6 +90,12 @@ case "$1" in
        PHX_FZ1=1 $J "pmc:r04_s25_c3_fz1_fetch:FETCH_SIZE:$B" "pmc:r04_s25_c3_fz1_write:WRITE_SIZE:$B" \
           "bench:r04_s25_bench_fz1a:$H" && $J "bench:r04_s25_bencha:$H" && PHX_FZ1=1 $J "bench:r04_s25_bench_fz1b:$H" && \
        $J "bench:r04_s25_benchb:$H" ;;
+  s26) # phx_lane_all with the interior point out of line; the single-change rule (C4, C3s8)
+       $J "test:tests/test_gpu_parity.py tests/test_trajectories.py tests/test_hydro.py" "bench:r04_s26_c4:--only C4 $A" \
+          "prof:r04_s26_c4_prof:--only C4 $A" "bench:r04_s26_c3s8:$S8" && \
+       PHX_LANE_DEFS=PHX_ALL_INLINE $J "bench:r04_s26_c4_inline:--only C4 $A" "bench:r04_s26_c3s8_inline:$S8" && \
+       PHX_LANE_DEFS=PHX_SINGLE_LARGEST $J "bench:r04_s26_c4_largest:--only C4 $A" "bench:r04_s26_c3s8_largest:$S8" && \
+       PHX_LANE_DEFS=PHX_SINGLE_DUAL_FIRST $J "bench:r04_s26_c4_dual:--only C4 $A" "bench:r04_s26_c3s8_dual:$S8" ;;
   final) # the round's evidence: the whole GPU suite, the driver's default command, kernel traces
        $J "test:tests" && $J "bench:r04_final_default:" "prof:r04_final_prof:$H --ar-probe 0" \
           "prof:r04_final_c3s8_prof:$S8" "prof:r04_final_1m_prof:$M" "prof:r04_final_c2_prof:--only C2 $A" \
