@@ -57,12 +57,13 @@ if os.environ.get("GC_FREEZE"):
 S = int(os.environ.get("SCENS", "100000"))
 w = {"names": farmer.scenario_names_creator, "creator": farmer.scenario_creator,
      "kw": lambda S, cm: {"num_scens": S, "crops_multiplier": cm}, "nodes": None}
+dev = bench.Dev(os.environ.get("DEV", "cuda"))
 for rep in range(2):
-    ph = bench.make_ph(w, S, 1, 1.0, {}, 20)
-    torch.cuda.synchronize()
+    ph = bench.make_ph(w, S, 1, 1.0, {}, 20, dev)
+    dev.sync()
     REC.clear()
     GC.clear()
-    T = bench.timed_run(ph, 20)
+    T = bench.timed_run(ph, 20, dev)
     print("run", rep, "T, T_iter0, T_iterk (ms):", ["%.3f" % (1e3 * v) for v in T])
     del ph
 t_first = min(r[0] for r in REC if r[3].endswith("Iter0"))
