@@ -96,6 +96,11 @@ case "$1" in
        PHX_LANE_DEFS=PHX_ALL_INLINE $J "bench:r04_s26_c4_inline:--only C4 $A" "bench:r04_s26_c3s8_inline:$S8" && \
        PHX_LANE_DEFS=PHX_SINGLE_LARGEST $J "bench:r04_s26_c4_largest:--only C4 $A" "bench:r04_s26_c3s8_largest:$S8" && \
        PHX_LANE_DEFS=PHX_SINGLE_DUAL_FIRST $J "bench:r04_s26_c4_dual:--only C4 $A" "bench:r04_s26_c3s8_dual:$S8" ;;
+  s27) # the loop's tail: copies enqueued with the last iteration, lazy counter resets; host wall timelines
+       $J "test:tests/test_gpu_parity.py tests/test_trajectories.py tests/test_hydro.py tests/test_engine_emu.py" \
+          "bench:r04_s27_c3s8:$S8" "bench:r04_s27_bench:$H" "prof:r04_s27_c3s8_prof:$S8" && \
+       SCENS=12500 timeout -k 10 200 python scripts/iter0_wall.py > gpurun_out/r04_s27_wall_12k5.txt 2>&1 && \
+       SCENS=100000 timeout -k 10 200 python scripts/iter0_wall.py > gpurun_out/r04_s27_wall_100k.txt 2>&1 ;;
   final) # the round's evidence: the whole GPU suite, the driver's default command, kernel traces
        $J "test:tests" && $J "bench:r04_final_default:" "prof:r04_final_prof:$H --ar-probe 0" \
           "prof:r04_final_c3s8_prof:$S8" "prof:r04_final_1m_prof:$M" "prof:r04_final_c2_prof:--only C2 $A" \
