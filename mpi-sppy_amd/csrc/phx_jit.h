@@ -324,7 +324,13 @@ inline std::string lane_kernel_source(const LaneStructure& L, int warm_waves = 1
          "  if (t < io.S) still = phx_lane::map_lane<PT>(io, t);\n"
          "  phx_lane::compact_lane(still, t, io.lanes_out, io.count_out);\n"
          "}\n";
-    o << "extern \"C\" __global__ void __launch_bounds__(64, " << warm_waves
+    // (the rescue list: a few per cent of the lanes, at most about one
+    // wavefront per SIMD -- the whole register file and every round on the
+    // data loaded at entry; PHX_LIST_RELOAD: the warm pass's build)
+    const std::string wlr = with_map ? "phx_lane::warm_lane<PT, true, true>" : "phx_lane::warm_lane<PT, false, true>";
+    o << "#ifdef PHX_LIST_RELOAD\n#define PHX_LIST_WAVES " << warm_waves << "\n#define PHX_LIST_FN " << wl
+      << "\n#else\n#define PHX_LIST_WAVES 1\n#define PHX_LIST_FN " << wlr << "\n#endif\n";
+    o << "extern \"C\" __global__ void __launch_bounds__(64, PHX_LIST_WAVES"
       << ") phx_lane_warm_list(phx_lane::LaneIO io, const int* lanes, const int* count) {\n"
          "  if (phx_lane::gated(io.gate)) return;\n"
          "  const int nl = *count;\n"
@@ -332,7 +338,7 @@ inline std::string lane_kernel_source(const LaneStructure& L, int warm_waves = 1
          "    const int t = base + threadIdx.x;\n"
          "    bool still = false;\n"
          "    int sc = -1;\n"
-         "    if (t < nl) { sc = lanes[t]; still = " + wl + "(io, sc); }\n"
+         "    if (t < nl) { sc = lanes[t]; still = PHX_LIST_FN(io, sc); }\n"
          "    phx_lane::compact_lane(still, sc, io.lanes_out, io.count_out);\n"
          "  }\n"
          "}\n";

@@ -1526,7 +1526,9 @@ PHX_LD void write_certified(const LaneIO& io, const Data<PT>& D, int sc, const A
 // ---------------------------------------------------------------------------
 // Kernel bodies.  Both return true if the lane still needs the generic path.
 // ---------------------------------------------------------------------------
-template <class PT, bool MAP = true>
+// REG: every round on the data loaded at entry (one wave per SIMD kernels with
+// the whole register file, phx_lane_warm_list: no per-round re-load)
+template <class PT, bool MAP = true, bool REG = false>
 PHX_LD bool warm_lane(const LaneIO& io, int sc) {
     constexpr int NN = PT::NMAX_N, MM = PT::NMAX_M;
     const Data<PT> D(io, sc);
@@ -1545,7 +1547,17 @@ PHX_LD bool warm_lane(const LaneIO& io, int sc) {
         }
         // the active set moved: rounds from the updated set, warm from (xp, z)
     }
-    if (as_rounds<PT>(io, sc, a, io.warm_rounds, xp, z)) {
+    if (REG) {
+        PHX_NOUNROLL for (int r = 0; r < io.warm_rounds; ++r) {
+            const int c = as_round<PT>(io, D, a, xp, z, r);
+            if (c == 0) {
+                const bool mok = MAP && io.map && map_compute<PT>(D, a, io, sc);
+                write_certified<PT>(io, D, sc, a, xp, z, 0, mok);
+                return false;
+            }
+            if (c != 1) { PHX_LANE_STAT(3); break; }
+        }
+    } else if (as_rounds<PT>(io, sc, a, io.warm_rounds, xp, z)) {
         const Data<PT> Dc(io, opaque_index(sc));
         const bool mok = MAP && io.map && map_compute<PT>(Dc, a, io, sc);
         write_certified<PT>(io, Dc, sc, a, xp, z, 0, mok);

@@ -100,7 +100,10 @@ case "$1" in
        $J "test:tests/test_gpu_parity.py tests/test_trajectories.py tests/test_hydro.py tests/test_engine_emu.py" \
           "bench:r04_s27_c3s8:$S8" "bench:r04_s27_bench:$H" "prof:r04_s27_c3s8_prof:$S8" && \
        SCENS=12500 timeout -k 10 200 python scripts/iter0_wall.py > gpurun_out/r04_s27_wall_12k5.txt 2>&1 && \
-       SCENS=100000 timeout -k 10 200 python scripts/iter0_wall.py > gpurun_out/r04_s27_wall_100k.txt 2>&1 ;;
+       SCENS=100000 timeout -k 10 200 python scripts/iter0_wall.py > gpurun_out/r04_s27_wall_100k.txt 2>&1 && \
+       $J "bench:r04_s27_1m:--only C3x1M --no-cpu-baseline --no-conv --steps 10 --warmup 1" && \
+       PHX_LANE_DEFS=PHX_LIST_RELOAD $J "bench:r04_s27_bench_reload:$H" \
+          "bench:r04_s27_1m_reload:--only C3x1M --no-cpu-baseline --no-conv --steps 10 --warmup 1" ;;
   final) # the round's evidence: the whole GPU suite, the driver's default command, kernel traces
        $J "test:tests" && $J "bench:r04_final_default:" "prof:r04_final_prof:$H --ar-probe 0" \
           "prof:r04_final_c3s8_prof:$S8" "prof:r04_final_1m_prof:$M" "prof:r04_final_c2_prof:--only C2 $A" \
