@@ -1692,12 +1692,18 @@ PHX_LD bool cold_rounds_lane(const LaneIO& io, int sc) {
 // true: the lane needs the generic path.
 template <class PT>
 PHX_LD bool all_lane(const LaneIO& io, int sc, int rescue) {
-    if (!warm_lane<PT, false>(io, sc)) return false;
+    // (the rounds on the data loaded at entry; PHX_ALL_RELOAD: re-loaded per round)
+#ifdef PHX_ALL_RELOAD
+    constexpr bool REG = false;
+#else
+    constexpr bool REG = true;
+#endif
+    if (!warm_lane<PT, false, REG>(io, sc)) return false;
     if (rescue > 0) {
         LaneIO io2 = io;
         io2.warm_rounds = rescue;
         io2.single_after = 1;
-        if (!warm_lane<PT, false>(io2, sc)) return false;
+        if (!warm_lane<PT, false, REG>(io2, sc)) return false;
     }
     LaneIO io3 = io;
     io3.single_after = 1;          // (the cold pass after warm passes: single changes, phx_kernels.hip)

@@ -103,7 +103,9 @@ case "$1" in
        SCENS=100000 timeout -k 10 200 python scripts/iter0_wall.py > gpurun_out/r04_s27_wall_100k.txt 2>&1 && \
        $J "bench:r04_s27_1m:--only C3x1M --no-cpu-baseline --no-conv --steps 10 --warmup 1" && \
        PHX_LANE_DEFS=PHX_LIST_RELOAD $J "bench:r04_s27_bench_reload:$H" \
-          "bench:r04_s27_1m_reload:--only C3x1M --no-cpu-baseline --no-conv --steps 10 --warmup 1" ;;
+          "bench:r04_s27_1m_reload:--only C3x1M --no-cpu-baseline --no-conv --steps 10 --warmup 1" && \
+       $J "bench:r04_s27_c4:--only C4 $A" "prof:r04_s27_c4_prof:--only C4 $A" && \
+       PHX_LANE_DEFS=PHX_ALL_RELOAD $J "bench:r04_s27_c3s8_allreload:$S8" "bench:r04_s27_c4_allreload:--only C4 $A" ;;
   final) # the round's evidence: the whole GPU suite, the driver's default command, kernel traces
        $J "test:tests" && $J "bench:r04_final_default:" "prof:r04_final_prof:$H --ar-probe 0" \
           "prof:r04_final_c3s8_prof:$S8" "prof:r04_final_1m_prof:$M" "prof:r04_final_c2_prof:--only C2 $A" \
