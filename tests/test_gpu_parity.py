@@ -513,3 +513,32 @@ def test_per_rank_slice_12500_gpu(gpu_lib):
     conv, E[obj] to 1e-9; the fused sums run in another fixed order)."""
     from test_engine_emu import check_native_vs_host
     check_native_vs_host(gpu_lib, None, "farmer", S=12500, fused=1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["farmer100k", "aircond1k"])
+def test_register_resident_rescue_rounds_gpu(gpu_lib, monkeypatch, case):
+    """The rescue-list kernel and phx_lane_all run their rounds on the data
+    loaded at entry (phx_lane.h warm_lane<.., REG>); the re-loading builds
+    (PHX_LIST_RELOAD, PHX_ALL_RELOAD) run the same arithmetic on the same
+    values: both give the same PH trajectory (farmer 100k: the first
+    iteration's rescue list; aircond 10x10x10: phx_lane_all's rescue rounds)."""
+    from mpisppy_amd.examples import aircond, farmer
+    from mpisppy_amd.utils import sputils
+    runs = []
+    for defs in ("", "PHX_LIST_RELOAD PHX_ALL_RELOAD"):
+        monkeypatch.setenv("PHX_LANE_DEFS", defs)
+        if case == "farmer100k":
+            S = 100000
+            r = run_engine(farmer.scenario_creator, farmer.scenario_names_creator(S), {"num_scens": S}, 3,
+                           lib=gpu_lib, device="cuda")
+        else:
+            bfs = [10, 10, 10]
+            r = run_engine(aircond.scenario_creator, ["scen%d" % i for i in range(1000)],
+                           {"branching_factors": bfs, "start_seed": 0}, 6, lib=gpu_lib, device="cuda",
+                           all_nodenames=sputils.create_nodenames_from_branching_factors(bfs))
+        assert all(s["not_optimal"] == 0 for s in r[0].solve_stats)
+        runs.append(r)
+    (a, ca, Ea, ta), (b, cb, Eb, tb) = runs
+    assert rel(a.W_array(), b.W_array()) < 1e-12
+    assert abs(Ea - Eb) <= 1e-12 * abs(Ea) and abs(ca - cb) <= 1e-12 * max(1.0, abs(ca))
