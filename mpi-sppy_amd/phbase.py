@@ -351,7 +351,11 @@ class PHBase(SPOpt):
         # tolerance is far above their rounding difference)
         E1 = getattr(self, "_E1_pre", None)
         if E1 is None:        # (host data, once: no device read in the timed Iter0)
-            E1 = float(np.sum(np.asarray(self.batch.prob, dtype=np.float64)))
+            pre = getattr(self, "_prob_local_sum", None)
+            if pre is not None and pre[0] == id(self.batch.prob):
+                E1 = pre[1]   # (summed at construction, spbase._look_and_leap)
+            else:
+                E1 = float(np.sum(np.asarray(self.batch.prob, dtype=np.float64)))
             if self.n_proc > 1:
                 E1 = float(self.mpicomm.allreduce_np(np.array([E1]), op="sum")[0])
             self._E1_pre = E1

