@@ -106,6 +106,9 @@ case "$1" in
           "bench:r04_s27_1m_reload:--only C3x1M --no-cpu-baseline --no-conv --steps 10 --warmup 1" && \
        $J "bench:r04_s27_c4:--only C4 $A" "prof:r04_s27_c4_prof:--only C4 $A" && \
        PHX_LANE_DEFS=PHX_ALL_RELOAD $J "bench:r04_s27_c3s8_allreload:$S8" "bench:r04_s27_c4_allreload:--only C4 $A" ;;
+  s28) # Iter0's E1 sum at construction (host)
+       $J "test:tests/test_gpu_parity.py tests/test_engine_emu.py" "bench:r04_s28_bench:$H" "bench:r04_s28_c3s8:$S8" \
+          "bench:r04_s28_1m:--only C3x1M --no-cpu-baseline --no-conv --steps 10 --warmup 1" ;;
   final) # the round's evidence: the whole GPU suite, the driver's default command, kernel traces
        $J "test:tests" && $J "bench:r04_final_default:" "prof:r04_final_prof:$H --ar-probe 0" \
           "prof:r04_final_c3s8_prof:$S8" "prof:r04_final_1m_prof:$M" "prof:r04_final_c2_prof:--only C2 $A" \
