@@ -109,6 +109,10 @@ case "$1" in
   s28) # Iter0's E1 sum at construction (host)
        $J "test:tests/test_gpu_parity.py tests/test_engine_emu.py" "bench:r04_s28_bench:$H" "bench:r04_s28_c3s8:$S8" \
           "bench:r04_s28_1m:--only C3x1M --no-cpu-baseline --no-conv --steps 10 --warmup 1" ;;
+  s29) # small batches: phx_lane_all against the separate passes (warm, register-resident rescue list, cold)
+       $J "bench:r04_s29_c4:--only C4 $A" "bench:r04_s29_c3s8:$S8" && \
+       PHX_NO_ALL=1 $J "bench:r04_s29_c4_noall:--only C4 $A" "bench:r04_s29_c3s8_noall:$S8" "prof:r04_s29_c4_noall_prof:--only C4 $A" && \
+       $J "bench:r04_s29_c4b:--only C4 $A" && PHX_NO_ALL=1 $J "bench:r04_s29_c4b_noall:--only C4 $A" ;;
   final) # the round's evidence: the whole GPU suite, the driver's default command, kernel traces
        $J "test:tests" && $J "bench:r04_final_default:" "prof:r04_final_prof:$H --ar-probe 0" \
           "prof:r04_final_c3s8_prof:$S8" "prof:r04_final_1m_prof:$M" "prof:r04_final_c2_prof:--only C2 $A" \
