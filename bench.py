@@ -491,6 +491,14 @@ def run_config(name, w, args, K, so, world, dev):
     """One secondary config at N = 1: Iter0 + K iterations on a fresh PH object."""
     S = w["S"]
     so = dict(so, **w.get("so", {}))
+    # warmup as the headline's: an untimed Iter0 + W iterations on its own
+    # object (each kernel's first launch -- code object load, the queue's
+    # scratch growth -- outside the timed run)
+    if args.warmup > 0:
+        ph = make_ph(w, S, 1, args.rho, so, args.warmup, dev)
+        ph.ph_main(finalize=False)
+        dev.sync()
+        del ph
     t = time.perf_counter()
     ph = make_ph(w, S, 1, args.rho, so, K, dev)
     dev.sync()
