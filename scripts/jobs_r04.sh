@@ -113,6 +113,11 @@ case "$1" in
        $J "bench:r04_s29_c4:--only C4 $A" "bench:r04_s29_c3s8:$S8" && \
        PHX_NO_ALL=1 $J "bench:r04_s29_c4_noall:--only C4 $A" "bench:r04_s29_c3s8_noall:$S8" "prof:r04_s29_c4_noall_prof:--only C4 $A" && \
        $J "bench:r04_s29_c4b:--only C4 $A" && PHX_NO_ALL=1 $J "bench:r04_s29_c4b_noall:--only C4 $A" ;;
+  s30) # the warm pass at one wave per SIMD with register-resident rounds (PHX_WARM_REG), A/B twice
+       $J "bench:r04_s30_bench:$H" && PHX_LANE_DEFS=PHX_WARM_REG $J "bench:r04_s30_bench_wreg:$H" \
+          "bench:r04_s30_1m_wreg:--only C3x1M --no-cpu-baseline --no-conv --steps 10 --warmup 1" && \
+       $J "bench:r04_s30_bench2:$H" "bench:r04_s30_1m:--only C3x1M --no-cpu-baseline --no-conv --steps 10 --warmup 1" && \
+       PHX_LANE_DEFS=PHX_WARM_REG $J "bench:r04_s30_bench_wreg2:$H" ;;
   final) # the round's evidence: the whole GPU suite, the driver's default command, kernel traces
        $J "test:tests" && $J "bench:r04_final_default:" "prof:r04_final_prof:$H --ar-probe 0" \
           "prof:r04_final_c3s8_prof:$S8" "prof:r04_final_1m_prof:$M" "prof:r04_final_c2_prof:--only C2 $A" \
