@@ -265,12 +265,7 @@ inline std::string lane_kernel_source(const LaneStructure& L, int warm_waves = 1
     // pass); phx_lane_warm_list: one more round over a compacted lane list
     // (the few lanes whose active set changed), so no wavefront idles while
     // one of its lanes needs a second round.
-    // (PHX_WARM_REG, experiment: one wave per SIMD and the rounds on the data
-    // loaded at entry, as the rescue list)
-    const std::string wlr0 = with_map ? "phx_lane::warm_lane<PT, true, true>" : "phx_lane::warm_lane<PT, false, true>";
-    o << "#ifdef PHX_WARM_REG\n#define PHX_WARM_WAVES 1\n#define PHX_WARM_FN " << wlr0
-      << "\n#else\n#define PHX_WARM_WAVES " << warm_waves << "\n#define PHX_WARM_FN " << wl << "\n#endif\n";
-    o << "extern \"C\" __global__ void __launch_bounds__(64, PHX_WARM_WAVES"
+    o << "extern \"C\" __global__ void __launch_bounds__(64, " << warm_waves
       << ") phx_lane_warm(phx_lane::LaneIO io) {\n"
          "  phx_lane::lane_stamp(io, 0);\n"
          "  if (phx_lane::gated(io.gate)) return;\n"
@@ -282,7 +277,7 @@ inline std::string lane_kernel_source(const LaneStructure& L, int warm_waves = 1
          "  if (t < io.S) {\n"
          "    if (io.fz.on) (void)phx_lane::fz_update_w<PT>(io, t);\n"
          "    phx_lane::lane_stamp(io, 2);\n"
-         "    still = PHX_WARM_FN(io, t);\n"
+         "    still = " + wl + "(io, t);\n"
          "  }\n"
          "  phx_lane::lane_stamp(io, 3);\n"
          "  phx_lane::compact_lane(still, t, io.lanes_out, io.count_out);\n"
