@@ -118,6 +118,10 @@ case "$1" in
           "bench:r04_s30_1m_wreg:--only C3x1M --no-cpu-baseline --no-conv --steps 10 --warmup 1" && \
        $J "bench:r04_s30_bench2:$H" "bench:r04_s30_1m:--only C3x1M --no-cpu-baseline --no-conv --steps 10 --warmup 1" && \
        PHX_LANE_DEFS=PHX_WARM_REG $J "bench:r04_s30_bench_wreg2:$H" ;;
+  s31) # workgroup round budgets: C5a (config default 4) and C2 (library default 16)
+       $J "bench:r04_s31_c5a_w3:--only C5a $A --so {\"wg_warm\":3}" "bench:r04_s31_c5a_w4:--only C5a $A" \
+          "bench:r04_s31_c5a_w6:--only C5a $A --so {\"wg_warm\":6}" "bench:r04_s31_c2_w8:--only C2 $A --so {\"wg_warm\":8}" \
+          "bench:r04_s31_c2_w16:--only C2 $A" "bench:r04_s31_c2_w24:--only C2 $A --so {\"wg_warm\":24}" ;;
   final) # the round's evidence: the whole GPU suite, the driver's default command, kernel traces
        $J "test:tests" && $J "bench:r04_final_default:" "prof:r04_final_prof:$H --ar-probe 0" \
           "prof:r04_final_c3s8_prof:$S8" "prof:r04_final_1m_prof:$M" "prof:r04_final_c2_prof:--only C2 $A" \
