@@ -122,6 +122,10 @@ case "$1" in
        $J "bench:r04_s31_c5a_w3:--only C5a $A --so {\"wg_warm\":3}" "bench:r04_s31_c5a_w4:--only C5a $A" \
           "bench:r04_s31_c5a_w6:--only C5a $A --so {\"wg_warm\":6}" "bench:r04_s31_c2_w8:--only C2 $A --so {\"wg_warm\":8}" \
           "bench:r04_s31_c2_w16:--only C2 $A" "bench:r04_s31_c2_w24:--only C2 $A --so {\"wg_warm\":24}" ;;
+  s32) # C2 round budget again (noise) and below
+       $J "bench:r04_s32_c2_w4:--only C2 $A --so {\"wg_warm\":4}" "bench:r04_s32_c2_w6:--only C2 $A --so {\"wg_warm\":6}" \
+          "bench:r04_s32_c2_w8:--only C2 $A --so {\"wg_warm\":8}" "bench:r04_s32_c2_w16:--only C2 $A" \
+          "bench:r04_s32_c2_w8b:--only C2 $A --so {\"wg_warm\":8}" "bench:r04_s32_c2_w16b:--only C2 $A" ;;
   final) # the round's evidence: the whole GPU suite, the driver's default command, kernel traces
        $J "test:tests" && $J "bench:r04_final_default:" "prof:r04_final_prof:$H --ar-probe 0" \
           "prof:r04_final_c3s8_prof:$S8" "prof:r04_final_1m_prof:$M" "prof:r04_final_c2_prof:--only C2 $A" \
