@@ -86,6 +86,8 @@ def parse():
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: test hook (gloo + the host emulation library, no GPU)")
     ap.add_argument("--so", default=None, help="extra solver options (JSON), e.g. '{\"seed_templates\": 0}'")
+    ap.add_argument("--detail", default=os.path.join(_ROOT, "bench_detail.json"),
+                    help="file for the full per-config record (stdout's last line is the compact headline)")
     ap.add_argument("--ar-probe", type=int, default=1,
                     help="N = 1: time phx_iterk with a no-op all-reduce callback (the per-iteration host "
                          "cost of the Python collective hook)")
@@ -264,6 +266,9 @@ def cpu_baseline(args, model="farmer", cm=1, scens=None, iters=None, total=None,
     if phys:
         out["whole_host"] = {"value": d["value"] * phys / d["cores"], "cores": phys, "sockets": host.get("sockets"),
                              "measured": False,
+                             "cap": "the GPU pool caps a one-GPU lease's worker pools at its CPU share (16 "
+                                    "processes; nproc shows all %s CPUs): P = %d physical cores not runnable here"
+                                    % (host.get("nproc"), phys),
                              "how": "per_gpu_share x physical cores / %d (perfect linear scaling: an upper bound "
                                     "on the host)" % d["cores"]}
     return out
@@ -665,9 +670,127 @@ def main():
                 res["configs"][nm] = {"error": repr(e)[:500]}
             print("[bench] %s done" % nm, file=sys.stderr, flush=True)
     if rank == 0:
-        print(json.dumps(res), flush=True)
+        # the full record (every config's workload, solver, PMC provenance, CPU
+        # sample text) goes to a file; stdout's LAST line is the compact headline
+        # the driver parses (<= LINE_CAP bytes; stderr stays short too: the
+        # driver keeps only the tail of both)
+        full = json.dumps(res)
+        try:
+            with open(args.detail, "w") as f:
+                f.write(full + "\n")
+            print("[bench] full record: %s (%d bytes)" % (args.detail, len(full)), file=sys.stderr, flush=True)
+        except OSError as e:
+            print("[bench] could not write %s: %r" % (args.detail, e), file=sys.stderr, flush=True)
+        print(json.dumps(compact_line(res, args.detail)), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+LINE_CAP = 8000     # bytes of the stdout headline line (the driver's parser: <= 8 KB)
+
+
+def _r(v, nd=4):
+    """Round a float to nd significant digits (compact line); other values as is."""
+    if isinstance(v, float):
+        return float("%.*g" % (nd, v))
+    return v
+
+
+def _roof_short(rf, full=True):
+    if not rf:
+        return None
+    keys = (["bound", "achieved", "peak", "unit", "frac", "traffic", "traffic_ratio", "kernel", "bytes_per_unit",
+             "units_per_launch", "algorithmic_bytes_per_launch", "avg_launch_us", "launches"] if full
+            else ["kernel", "frac", "traffic_ratio", "avg_launch_us"])
+    out = {k: _r(rf.get(k)) for k in keys if k in rf}
+    if full:
+        out["traffic_unit"] = "bytes/launch"
+        out["traffic_source"] = rf.get("traffic_source")
+        st = rf.get("traffic_status") or ""
+        out["traffic_current"] = st.startswith("current")
+        v = rf.get("valu")
+        if isinstance(v, dict) and not v.get("stale"):
+            out["valu"] = {k: _r(v.get(k)) for k in ("valu_insts_per_wave", "waves_per_launch", "busiest_simd_waves",
+                                                   "issue_bound_us", "frac", "source")}
+    return out
+
+
+def _cpu_short(cb, full=True):
+    if not cb or "value" not in cb:
+        return cb
+    out = {"value": _r(cb["value"]), "unit": cb.get("unit"), "cores": cb.get("cores"), "kind": cb.get("kind")}
+    if full:
+        out["sample"] = (cb.get("sample") or "")[:240]
+        out["seconds"] = _r(cb.get("seconds"))
+        out["cpu_model"] = cb.get("cpu_model")
+        wh = cb.get("whole_host")
+        if wh:
+            out["whole_host"] = {k: _r(wh.get(k)) for k in ("value", "cores", "measured", "cap", "how") if k in wh}
+            if isinstance(out["whole_host"].get("how"), str):
+                out["whole_host"]["how"] = out["whole_host"]["how"][:200]
+        if cb.get("scaling"):
+            out["scaling"] = cb["scaling"]
+    return out
+
+
+def compact_line(res, detail_path):
+    """The driver-readable headline: BASELINE's metric and the contract keys, the
+    dominant kernel's roofline (traffic, ratio, VALU issue), the CPU baseline,
+    conv_time, Iter0 / steady, and per config value / ms_per_step / frac /
+    traffic_ratio / CPU value / avg_launch_us.  Everything else is in the detail
+    file.  Falls back to fewer keys if a field ever makes it longer than LINE_CAP."""
+    keep = ["metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data"]
+    out = {k: _r(res[k], 6) if k in ("value", "ms_per_step") else res[k] for k in keep if k in res}
+    c = res.get("config", {})
+    out["config"] = {k: c.get(k) for k in ("workload", "scenarios", "scenarios_per_gpu", "n", "m", "nonants", "rho",
+                                           "parallelism") if k in c}
+    out["T_s"] = _r(res.get("T_s"), 5)
+    out["iter0_s"] = _r(res.get("iter0_s"), 4)
+    st = res.get("steady") or {}
+    out["steady"] = {"value": _r(st.get("value")), "ms_per_step": _r(st.get("ms_per_step"))}
+    out["roofline"] = _roof_short(res.get("roofline"))
+    if "cpu_baseline" in res:
+        out["cpu_baseline"] = _cpu_short(res["cpu_baseline"])
+    if "conv_time" in res:
+        ct = res["conv_time"]
+        out["conv_time"] = {"seconds": _r(ct.get("seconds")), "iterations": ct.get("iterations"),
+                            "converged": ct.get("converged"), "convthresh": ct.get("convthresh")}
+    if res.get("iterk"):
+        out["iterk"] = res["iterk"]
+    out["not_optimal"] = res.get("not_optimal")
+    if "device" in res:
+        out["device"] = res["device"]
+    if "final" in res:
+        f = res["final"]
+        out["final"] = {"xbar": f.get("xbar"), "conv": f.get("conv"), "trivial_bound": f.get("trivial_bound")}
+    if res.get("configs"):
+        cs = {}
+        for nm, cr in res["configs"].items():
+            if "error" in cr:
+                cs[nm] = {"error": cr["error"][:120]}
+                continue
+            cst = cr.get("steady") or {}
+            rf = cr.get("roofline") or {}
+            cb = cr.get("cpu_baseline") or {}
+            cs[nm] = {"S": cr.get("scenarios"), "value": _r(cr.get("value")), "ms_per_step": _r(cst.get("ms_per_step")),
+                      "iter0_s": _r(cr.get("iter0_s"), 3), "kernel": rf.get("kernel"), "frac": _r(rf.get("frac"), 3),
+                      "traffic_ratio": _r(rf.get("traffic_ratio"), 3), "avg_launch_us": _r(rf.get("avg_launch_us")),
+                      "cpu": _r(cb.get("value")) if isinstance(cb, dict) else None,
+                      "stops": (cr.get("iterk") or {}).get("straggler_stops"), "not_optimal": cr.get("not_optimal")}
+        out["configs"] = cs
+    out["detail"] = os.path.relpath(detail_path, _ROOT) if os.path.isabs(detail_path) else detail_path
+    line = json.dumps(out)
+    # shed the least important fields if the line ever outgrows the cap
+    for drop in (("final",), ("iterk",), ("configs",)):
+        if len(line.encode()) <= LINE_CAP:
+            break
+        for k in drop:
+            out.pop(k, None)
+        line = json.dumps(out)
+    if len(line.encode()) > LINE_CAP and out.get("cpu_baseline"):
+        out["cpu_baseline"] = _cpu_short(res["cpu_baseline"], full=False)
+    return out
 
 
 if __name__ == "__main__":

@@ -1641,8 +1641,15 @@ PHX_LD bool cold_rounds_lane(const LaneIO& io, int sc) {
 #ifndef PHX_COLD_TRIES
 #define PHX_COLD_TRIES 3
 #endif
+    // (each retry strictly looser than the attempt before: one at or below it
+    // would repeat the classification that already cycled, a whole round
+    // budget for nothing)
+    double prev_tol = 0.0;
     for (int attempt = 0; attempt < PHX_COLD_TRIES && err < 1e-4; ++attempt) {
-        const double tol = attempt == 0 ? fmin(1e-4, fmax(1e-9, 10.0 * err)) : (attempt == 1 ? 1e-6 : 1e-4);
+        const double tol = attempt == 0 ? fmin(1e-4, fmax(1e-9, 10.0 * err))
+                                        : (attempt == 1 ? fmin(1e-4, fmax(1e-6, 10.0 * prev_tol)) : 1e-4);
+        if (attempt > 0 && !(tol > prev_tol)) continue;
+        prev_tol = tol;
         ASet<PT> a;
         {
             const Data<PT> D(io, sc);
@@ -1707,7 +1714,9 @@ PHX_LD bool all_lane(const LaneIO& io, int sc, int rescue) {
     }
     LaneIO io3 = io;
     io3.single_after = 1;          // (the cold pass after warm passes: single changes, phx_kernels.hip)
-    if (rescue > io3.as_rounds) io3.as_rounds = rescue;   // as enqueue_lane_solve's cold pass
+    // the rounds after the classification get the rescue budget, as every cold
+    // pass of enqueue_lane_solve (and the emulation's)
+    if (io3.as_rounds > 0 && rescue > io3.as_rounds) io3.as_rounds = rescue;
     ipm_lane<PT>(io3, sc);
     return cold_rounds_lane<PT>(io3, sc);
 }

@@ -349,16 +349,20 @@ class PHBase(SPOpt):
         # iteration (phbase.py:812-817): checked here, so a deferred Iter0
         # never runs iterations first (the same sum the device computes; the
         # tolerance is far above their rounding difference)
-        E1 = getattr(self, "_E1_pre", None)
-        if E1 is None:        # (host data, once: no device read in the timed Iter0)
+        # (host data, once per probability array: no device read in the timed
+        # Iter0; both caches hold the array they summed and compare with `is`)
+        pre_E1 = getattr(self, "_E1_pre", None)
+        if pre_E1 is not None and pre_E1[0] is self.batch.prob:
+            E1 = pre_E1[1]
+        else:
             pre = getattr(self, "_prob_local_sum", None)
-            if pre is not None and pre[0] == id(self.batch.prob):
+            if pre is not None and pre[0] is self.batch.prob:
                 E1 = pre[1]   # (summed at construction, spbase._look_and_leap)
             else:
                 E1 = float(np.sum(np.asarray(self.batch.prob, dtype=np.float64)))
             if self.n_proc > 1:
                 E1 = float(self.mpicomm.allreduce_np(np.array([E1]), op="sum")[0])
-            self._E1_pre = E1
+            self._E1_pre = (self.batch.prob, E1)
         if abs(1 - E1) > self.E1_tolerance:
             return False
         saved = self.current_solver_options
@@ -630,8 +634,10 @@ class PHBase(SPOpt):
         lib.check(self._ctx, lib.iterk(self._ctx, ctypes.byref(so), ctypes.byref(a), ctypes.byref(res),
                                        self._stream()), "iterk")
         if deferred:
-            if res.adopted:
+            if res.adopted and self._solve_pending:
                 # Iter0's solve, finished inside phx_iterk (phx_last_solve_stats: its statistics)
+                # (the host emulation finishes a deferred solve without
+                # leftovers at once: recorded then, adopted with none)
                 self._solve_pending = False
                 self._record_solve(self.solve_stats[-1], 0, int(res.adopted_stragglers))
             self._resolve_deferred_iter0(device_sums=bool(res.adopted))

@@ -168,11 +168,14 @@ class SPBase:
                 probs[k] = 1.0 / S
             else:
                 probs[k] = float(p)
+        # (read-only from here: the cached sum below stays valid)
+        probs.flags.writeable = False
         self.batch.prob = probs
         # the local probability sum, once (host data fixed from here): Iter0's
         # E1 check reads it instead of summing S values in the timed Iter0
-        # (phbase.py _can_defer_iter0; keyed by the array it summed)
-        self._prob_local_sum = (id(probs), float(np.sum(probs)))
+        # (phbase.py _can_defer_iter0; keyed by the array object it summed --
+        # held here, so a replacement array can never pass for it)
+        self._prob_local_sum = (probs, float(np.sum(probs)))
 
     def _set_sense(self):
         senses = self.mpicomm.allgather_object(self.batch.sense)

@@ -1,0 +1,17 @@
+#!/bin/bash
+# Round-5 GPU evidence jobs (run through gpurun): bash scripts/jobs_r05.sh <name>.
+# Each job is a list of scripts/gpu_job.sh steps; logs land in gpurun_out/, the
+# summaries judged are copied into profiles/ (named after the job).
+set -o pipefail
+B="--configs none --no-cpu-baseline --no-conv --steps 50"                 # headline, K = 50
+H="--configs none --no-cpu-baseline --no-conv"                            # headline, K = 20 (driver shape)
+M="--only C3x1M --no-cpu-baseline --no-conv --steps 20 --warmup 1 --ar-probe 0"   # over-cache 1M
+A="--no-cpu-baseline --no-conv --steps 10 --warmup 1"                     # one secondary config
+S8="--only C3s8 --no-cpu-baseline --no-conv --steps 20"                   # the 8-GPU per-rank slice
+SQ="SQ_INSTS_VALU,SQ_ACTIVE_INST_VALU,SQ_WAVE_CYCLES,SQ_WAIT_ANY,SQ_INSTS_VALU_FLOPS_FP64,SQ_INSTS_SALU"
+J="bash scripts/gpu_job.sh"
+case "$1" in
+  s1)  # the whole GPU suite, then the driver's default command (compact line)
+       $J "test:tests" && $J "bench:r05_s1_default:--detail gpurun_out/r05_s1_default_detail.json" ;;
+  *) echo "unknown job $1"; exit 2 ;;
+esac

@@ -14,16 +14,43 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _bench(n):
+def _bench(n, extra=("--no-conv", "--no-cpu-baseline", "--configs", "none"), tmp=None):
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
     env["OMP_NUM_THREADS"] = "1"
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--device", "cpu", "--scens", "600",
-           "--steps", "3", "--warmup", "1", "--no-conv", "--no-cpu-baseline", "--configs", "none", "--ar-probe", "0"]
+           "--steps", "3", "--warmup", "1", "--ar-probe", "0"] + list(extra)
+    if tmp is not None:
+        cmd += ["--detail", str(tmp)]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]          # rank 0 prints the one JSON line
-    return json.loads(lines[0])
+    last = r.stdout.rstrip("\n").splitlines()[-1]
+    assert last == lines[0]                            # ... as stdout's LAST line
+    assert len(last.encode()) <= 8192, len(last.encode())
+    return json.loads(last)
+
+
+def test_bench_line_compact_cpu(tmp_path):
+    """The driver parses stdout's last line (<= 8 KB): the contract keys, the roofline,
+    the CPU baseline, conv_time and a per-config summary; the full record goes to
+    the --detail file."""
+    detail = tmp_path / "detail.json"
+    d = _bench(1, extra=("--configs", "C1,C4", "--config-steps", "2", "--cpu-scens", "60", "--cpu-iters", "1",
+                         "--cpu-procs", "2", "--conv-max-iters", "50"), tmp=detail)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "dtype", "config", "roofline",
+              "cpu_baseline", "conv_time", "iter0_s", "steady", "configs"):
+        assert k in d, k
+    assert d["roofline"]["kernel"] and "frac" in d["roofline"] and "traffic_ratio" in d["roofline"]
+    assert d["cpu_baseline"]["value"] > 0 and d["cpu_baseline"]["cores"] == 2
+    for nm in ("C1", "C4"):
+        c = d["configs"][nm]
+        assert "error" not in c, c
+        for k in ("value", "ms_per_step", "frac", "traffic_ratio", "cpu", "avg_launch_us"):
+            assert k in c, (nm, k)
+    full = json.loads(detail.read_text())
+    assert full["configs"]["C4"]["workload"].startswith("aircond")
+    assert full["value"] == d["value"] or abs(full["value"] - d["value"]) <= 1e-5 * full["value"]
 
 
 def test_bench_launches_ranks_cpu():

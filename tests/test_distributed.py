@@ -85,3 +85,55 @@ def test_ranks_match_one(emu, case):
     assert [len(r[3]) for r in rs] == [int((g + 1) * S / world) - int(g * S / world) for g in range(world)]
     W = np.vstack([r[3] for r in rs])
     assert np.allclose(W, ph.W_array(), rtol=1e-10, atol=1e-9)
+
+
+def _worker_infeasible(rank, world, port, out):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import mpisppy_amd  # noqa: F401
+    from mpisppy_amd import _native
+    from mpisppy_amd.comm import Comm
+    from mpisppy_amd.opt.ph import PH
+    from mpisppy_amd.examples import farmer
+    from helpers import ph_options
+    from test_engine_emu import infeasible_farmer_creator
+    emu = _native.Lib(os.path.join(ROOT, "tests", "emu", "libphx_emu.so"), prefix="emu_phx_")
+    S = 30
+    ph = PH(ph_options(20), farmer.scenario_names_creator(S), infeasible_farmer_creator,
+            scenario_creator_kwargs={"num_scens": S}, _native_lib=emu, _device="cpu", mpicomm=Comm())
+    seen = []
+    orig = ph._native.iterk
+
+    def spy(ctx, so, a, res, stream):
+        rc = orig(ctx, so, a, res, stream)
+        seen.append((res._obj.iters, res._obj.solves, res._obj.adopted, res._obj.not_optimal))
+        return rc
+    ph._native.iterk = spy
+    quit_ = False
+    try:
+        ph.ph_main()
+    except SystemExit:
+        quit_ = True
+    out[rank] = (quit_, seen, len(ph.local_scenario_names))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_infeasible_deferred_iter0_two_ranks(emu):
+    """the deferred Iter0 adopted by phx_iterk with an
+    infeasible scenario on ONE rank: the stop decision is all-reduced, so both
+    ranks leave the device loop before any PH iteration and quit together
+    (phbase.py:812-823) instead of one rank waiting in iteration 1's all-reduce."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker_infeasible, args=(2, _free_port(), out), nprocs=2, join=True)
+    for r in range(2):
+        quit_, seen, nloc = out[r]
+        assert quit_, r
+        assert nloc == 15
+        assert [s[:3] for s in seen] == [(0, 0, 1)], (r, seen)
+    assert out[0][1][0][3] == 1 and out[1][1][0][3] == 0      # the infeasible scenario is rank 0's
