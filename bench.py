@@ -441,6 +441,9 @@ def dominant_kernel(ph, K, fused):
                 # (the one-wave build at every size unless PHX_FZ2=1, phx_kernels.hip)
                 fz2 = os.environ.get("PHX_FZ2") == "1"
                 kname = "phx_lane_warm_fz" if (fz2 and not small) else "phx_lane_warm_fz1"
+                # (the compacting build, phx_kernels.hip, unless PHX_FZC=0 / PHX_FZ_LEGACY=1)
+                if os.environ.get("PHX_FZC") != "0" and os.environ.get("PHX_FZ_LEGACY") != "1":
+                    kname = "phx_lane_warm_fzc"
             else:
                 kname = "phx_lane_all" if small else "phx_lane_warm"
             return (kname, st["lane_warm_ms"] / 1e3 / st["warm_launches"], st["warm_launches"],
@@ -494,7 +497,7 @@ def roofline(kernel, avg_s, launches, bpu, units, traffic=None, traffic_src=None
 # how phx_iterk's events time the dominant kernel (bench --timing-every < 0)
 LAUNCH_TIMING = {k: ("one HIP event pair around all the fused launches of the timed loop (back to back on "
                      "phx_iterk's stream; no per-launch records in between)")
-                 for k in ("phx_lane_warm_fz", "phx_lane_warm_fz1")}
+                 for k in ("phx_lane_warm_fz", "phx_lane_warm_fz1", "phx_lane_warm_fzc")}
 
 
 def run_config(name, w, args, K, so, world, dev):

@@ -300,6 +300,12 @@ inline std::string lane_kernel_source(const LaneStructure& L, int warm_waves = 1
          "  phx_lane::warm_fused<PT, true>(io);\n"
          "#endif\n"
          "}\n";
+    // ... compacting: round 0 per lane, the later rounds of the lanes that need
+    // them packed into full wavefronts by each group's last block (phx_lane.h
+    // warm_fused_c)
+    o << "extern \"C\" __global__ void __launch_bounds__(64, 1) phx_lane_warm_fzc(phx_lane::LaneIO io) {\n"
+         "  phx_lane::warm_fused_c<PT>(io);\n"
+         "}\n";
     // a whole warm solve (warm rounds, rescue rounds, interior point) in one
     // launch, for batches of at most one wavefront per SIMD (phx_lane.h all_lane)
     o << "extern \"C\" __global__ void __launch_bounds__(64, 1) phx_lane_all(phx_lane::LaneIO io, int rescue) {\n"

@@ -147,6 +147,16 @@ struct FusedW {
     int32_t g, R;              // this rank's emulated-rank entry, emulated rank count
     const double* cnt;         // [R] element counts (convergence_diff's denominators)
     double thresh;
+    // compacting mode (kernel phx_lane_warm_fzc, warm_fused_c): round 0 in every
+    // lane; the lanes it leaves with a changed active set are finished by the
+    // last block of their group of chunks (64-lane blocks), so no wavefront runs
+    // later rounds for one lane while 63 wait
+    double* rx;                // [n][S] a rework lane's x after round 0
+    double* rz;                // [m][S] ... and z
+    unsigned long long* rmask; // [blocks] rework lanes of each block
+    double* gpart;             // [groups * NV] the groups' rework-lane partials
+    unsigned int* gcnt;        // [groups] arrival counters (reset by each group's finisher)
+    int32_t gsize;             // blocks per group
 };
 
 // Runtime inputs/outputs (device pointers; per-scenario arrays [i*S + s]).
@@ -2193,6 +2203,295 @@ __device__ void warm_fused(const LaneIO& io) {
     lane_stamp(io, 4);
     fz_fold<PT>(io, v);
     lane_stamp(io, 5);
+}
+
+// ---------------------------------------------------------------------------
+// The compacting fused iteration (kernel phx_lane_warm_fzc).  A wavefront's
+// time is its slowest lane's: in steady PH iterations ~6 % of the lanes need a
+// second active-set round, so nearly every wavefront of warm_fused runs two
+// or more rounds for one or two lanes.  Here every block (64 lanes = one
+// chunk) runs Update_W and round 0 only; a lane that round 0 leaves with a
+// changed active set stashes (xp, z) and its active set, and the LAST block
+// of its group (gsize consecutive chunks, told by an arrival counter) runs the
+// remaining rounds for the group's rework lanes packed into full wavefronts
+// (scenario order: a deterministic assignment), from the very state a single
+// wavefront would have continued with -- the same data bits (Data from the
+// stored W, rho, A values and stage x-bar), the same round numbers, so the
+// same x, y, objective and active set per lane as warm_fused.  Only the x-bar
+// fold differs in order: the blocks' partials (round-0 lanes and every lane's
+// convergence term) folded as in fz_fold, then the groups' rework partials in
+// group order -- fixed orders, bitwise reproducible run to run.
+// Hand-offs (stash -> group finisher, partials -> last block): Guideline 16
+// R1 (write-through stores drained before one relaxed ticket; the consumer's
+// agent acquire), as fz_fold's.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void store_wt_u64(unsigned long long* p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long load_wt_u64(const unsigned long long* p) {
+    return __hip_atomic_load(const_cast<unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long readlane_u64(unsigned long long u, int l) {
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u & 0xffffffffull), l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), l);
+    return ((unsigned long long)hi << 32) | lo;
+}
+// the position of the r-th (0-based) set bit of w (w has more than r set bits)
+__device__ __forceinline__ int nth_set_bit(unsigned long long w, int r) {
+    for (int k = 0; k < r; ++k) w &= w - 1ull;
+    return (int)__builtin_ctzll(w);
+}
+
+// The rework lanes of group g (every lane of the block calls it): packed in
+// scenario order into wavefront batches; each lane continues its solve from
+// round 1.  gacc: the batches' partials [sum pc x | sum pc x^2] in batch order.
+template <class PT>
+__device__ void fz_rework_group(const LaneIO& io, int g, double* gacc) {
+    const FusedW& f = io.fz;
+    constexpr int NS = PT::nslot() > 0 ? PT::nslot() : 1;
+    constexpr int NV = 2 * NS + 1;
+    constexpr int NVA = PT::NMAX_V, NW = aset_words(PT::NMAX_N, PT::NMAX_M);
+    const int64_t S = io.S;
+    const int nch = (io.S + 63) / 64;
+    const int c0 = g * f.gsize;
+    const int ng = min(f.gsize, nch - c0);          // (<= 64: phx_kernels.hip caps gsize)
+    const int l = threadIdx.x;
+    const unsigned long long mine = l < ng ? load_wt_u64(&f.rmask[c0 + l]) : 0ull;
+    // inclusive prefix of the chunks' rework counts over the lanes
+    int inc = __popcll(mine);
+    PHX_UNROLL for (int d = 1; d < 64; d <<= 1) {
+        const int o = __shfl_up(inc, d, 64);
+        if (l >= d) inc += o;
+    }
+    const int total = __builtin_amdgcn_readlane(inc, 63);
+    const int exc = inc - __popcll(mine);
+    PHX_UNROLL for (int e = 0; e < NV; ++e) gacc[e] = 0.0;
+    for (int base = 0; base < total; base += 64) {
+        const int q = base + l;
+        int sc = -1;
+        for (int j = 0; j < ng; ++j) {              // wave-uniform: the chunk holding rank q
+            const int ej = __builtin_amdgcn_readlane(exc, j), ij = __builtin_amdgcn_readlane(inc, j);
+            if (ij > ej && q >= ej && q < ij) sc = (c0 + j) * 64 + nth_set_bit(readlane_u64(mine, j), q - ej);
+        }
+        bool still = false;
+        double v[NV];
+        PHX_UNROLL for (int e = 0; e < NV; ++e) v[e] = 0.0;
+        if (sc >= 0) {
+            double av[NVA], wv[NS], rv[NS], xb[NS], pcv[NS];
+            uint32_t aw[NW];
+            PHX_UNROLL for (int k = 0; k < PT::nvar(); ++k) av[k] = io.Av[(int64_t)k * S + sc];
+            PHX_UNROLL for (int k = 0; k < aset_words(PT::n(), PT::m()); ++k) aw[k] = io.aset[(int64_t)k * S + sc];
+            PHX_UNROLL for (int t = 0; t < PT::nslot(); ++t) {
+                const int64_t o = (int64_t)t * S + sc;
+                wv[t] = io.W[o];
+                rv[t] = io.rho[o];
+                pcv[t] = f.pc[o];
+                xb[t] = f.stage[t];
+            }
+            double xp[PT::NMAX_N], z[PT::NMAX_M];
+            PHX_UNROLL for (int j = 0; j < PT::n(); ++j) xp[j] = f.rx[(int64_t)j * S + sc];
+            PHX_UNROLL for (int i = 0; i < PT::m(); ++i) z[i] = f.rz[(int64_t)i * S + sc];
+            ASet<PT> a;
+            aset_from_words<PT>(aw, a);
+            const Data<PT> D(io, sc, av, wv, rv, xb);
+            int c = 1;
+            PHX_NOUNROLL for (int r = 1; r < io.warm_rounds && c == 1; ++r) c = as_round<PT>(io, D, a, xp, z, r);
+            if (c == 0) {
+                write_certified<PT>(io, D, sc, a, xp, z, 0);
+                PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
+                    const int t = PT::col_slot(j);
+                    if (t >= 0) {
+                        const double xn = xp[j] * (PT::scaled() ? PT::dcs(j) : 1.0);
+                        const double w = pcv[t] * xn;
+                        v[t] += w;
+                        v[NS + t] += w * xn;
+                    }
+                }
+            } else {
+                if (c == 2) PHX_LANE_STAT(3);
+                aset_store<PT>(io, sc, a);   // the updated active set seeds the next pass
+                io.status[sc] = 0;
+                io.flags[sc] = 0;
+                still = true;
+            }
+        }
+        compact_lane(still, sc, io.lanes_out, io.count_out);
+        PHX_UNROLL for (int e = 0; e < NV; ++e) gacc[e] += wave_sum(v[e]);
+    }
+}
+
+// fz_fold with the groups: the block's partial, its group arrival (the last
+// block of the group finishes the group's rework lanes), then the sharded
+// block arrival; the last block overall folds the shards, then the groups.
+template <class PT>
+__device__ void fz_fold_c(const LaneIO& io, double* v) {
+    const FusedW& f = io.fz;
+    constexpr int NS = PT::nslot() > 0 ? PT::nslot() : 1;
+    constexpr int NV = 2 * NS + 1;
+    PHX_UNROLL for (int e = 0; e < NV; ++e) v[e] = wave_sum(v[e]);
+    const unsigned nb = gridDim.x, b = blockIdx.x, k = b % TICKET_SHARDS;
+    const unsigned nk = (nb - k + TICKET_SHARDS - 1) / TICKET_SHARDS;
+    const unsigned nsh = nb < TICKET_SHARDS ? nb : TICKET_SHARDS;
+    const unsigned gs = (unsigned)f.gsize, g = b / gs;
+    const unsigned gn = (nb - g * gs) < gs ? (nb - g * gs) : gs;
+    double* shard_part = f.part + (int64_t)nb * NV;
+    __shared__ unsigned s_state;
+    if (threadIdx.x == 0) {
+        PHX_UNROLL for (int e = 0; e < NV; ++e) store_wt(&f.part[(int64_t)b * NV + e], v[e]);
+        // (this wavefront's stash, W and active-set stores: all write-through,
+        // drained here with the partials before the group ticket)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        PHX_HANDOFF_RELEASE();
+        s_state = __hip_atomic_fetch_add(f.gcnt + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gn - 1u;
+    }
+    __syncthreads();
+    if (s_state) {
+        PHX_HANDOFF_ACQUIRE();
+        if (threadIdx.x == 0) __hip_atomic_store(f.gcnt + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        double ga[NV];
+        fz_rework_group<PT>(io, (int)g, ga);
+        if (threadIdx.x == 0)
+            PHX_UNROLL for (int e = 0; e < NV; ++e) store_wt(&f.gpart[(int64_t)g * NV + e], ga[e]);
+    }
+    if (threadIdx.x == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        PHX_HANDOFF_RELEASE();
+        s_state = __hip_atomic_fetch_add(f.tk + k * TICKET_STRIDE, 1u, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT) == nk - 1u;
+    }
+    __syncthreads();
+    if (!s_state) return;
+    PHX_HANDOFF_ACQUIRE();
+    // last of shard k: blocks k, k+8, ... in order (4 blocks' loads in flight)
+    PHX_UNROLL for (int e = 0; e < NV; ++e) v[e] = 0.0;
+    for (unsigned i0 = threadIdx.x; i0 < nk; i0 += 4 * 64) {
+        double l[4][NV];
+        PHX_UNROLL for (int u = 0; u < 4; ++u) {
+            const unsigned i = i0 + 64u * u;
+            PHX_UNROLL for (int e = 0; e < NV; ++e)
+                l[u][e] = i < nk ? load_wt(&f.part[(int64_t)(k + TICKET_SHARDS * i) * NV + e]) : 0.0;
+        }
+        PHX_UNROLL for (int u = 0; u < 4; ++u) PHX_UNROLL for (int e = 0; e < NV; ++e) v[e] += l[u][e];
+    }
+    PHX_UNROLL for (int e = 0; e < NV; ++e) v[e] = wave_sum(v[e]);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        PHX_UNROLL for (int e = 0; e < NV; ++e) store_wt(&shard_part[k * NV + e], v[e]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        PHX_HANDOFF_RELEASE();
+        const bool last = __hip_atomic_fetch_add(f.tk + TICKET_SHARDS * TICKET_STRIDE, 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT) == nsh - 1u;
+        if (last)
+            for (int q = 0; q <= TICKET_SHARDS; ++q) f.tk[q * TICKET_STRIDE] = 0u;
+        s_state = last ? 2u : 0u;
+    }
+    __syncthreads();
+    if (s_state != 2u) return;
+    PHX_HANDOFF_ACQUIRE();
+    // the last block overall: the groups' rework partials (lane-strided, then
+    // the wave sum), then the shards in order + the groups: iteration k+1's stage
+    const unsigned ngr = (nb + gs - 1) / gs;
+    double gsum[NV];
+    PHX_UNROLL for (int e = 0; e < NV; ++e) gsum[e] = 0.0;
+    for (unsigned q = threadIdx.x; q < ngr; q += 64)
+        PHX_UNROLL for (int e = 0; e < NV; ++e) gsum[e] += load_wt(&f.gpart[(int64_t)q * NV + e]);
+    PHX_UNROLL for (int e = 0; e < NV; ++e) gsum[e] = wave_sum(gsum[e]);
+    const int e = threadIdx.x;
+    if (e < NV) {
+        double a = 0.0;
+        for (unsigned q = 0; q < nsh; ++q) a += load_wt(&shard_part[q * NV + e]);
+        double ge = 0.0;
+        PHX_UNROLL for (int u = 0; u < NV; ++u) ge = u == e ? gsum[u] : ge;
+        a += ge;
+        if (e < NS) f.stage[e] = a;
+        else if (e < 2 * NS) f.stage[f.nns + (e - NS)] = a;
+        else {
+            for (int r = 0; r < f.R; ++r) f.stage[2 * f.nns + 1 + r] = r == f.g ? a : 0.0;
+            f.stage[2 * f.nns] =
+                (double)__hip_atomic_load(io.count_out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+template <class PT>
+__device__ void warm_fused_c(const LaneIO& io) {
+    const FusedW& f = io.fz;
+    constexpr int NS = PT::nslot() > 0 ? PT::nslot() : 1;
+    constexpr int NV = 2 * NS + 1;
+    constexpr int NVA = PT::NMAX_V, NW = aset_words(PT::NMAX_N, PT::NMAX_M);
+    const int sc = blockIdx.x * 64 + threadIdx.x;
+    const bool live = sc < io.S;
+    const int s = live ? sc : 0;            // (tail lanes load lane 0's values: valid addresses, unused)
+    const int64_t S = io.S;
+    double av[NVA], xv[NS], wv[NS], rv[NS], pcv[NS];
+    uint32_t aw[NW];
+    PHX_UNROLL for (int v = 0; v < PT::nvar(); ++v) av[v] = io.Av[(int64_t)v * S + s];
+    PHX_UNROLL for (int k = 0; k < aset_words(PT::n(), PT::m()); ++k) aw[k] = io.aset[(int64_t)k * S + s];
+    PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
+        const int t = PT::col_slot(j);
+        if (t >= 0) {
+            const int64_t o = (int64_t)t * S + s;
+            xv[t] = f.x_prev[(int64_t)j * S + s];
+            wv[t] = io.W[o];
+            rv[t] = io.rho[o];
+            pcv[t] = f.pc[o];
+        }
+    }
+    if (gated(io.gate)) return;
+    if (!fz_prologue(io)) return;
+    zero_next_counts(io.counts_next);
+    // Update_W (phbase.py:293-318) and |x_{k-1} - x-bar_k| (convergence_diff)
+    double xb[NS], dl = 0.0;
+    PHX_UNROLL for (int t = 0; t < PT::nslot(); ++t) {
+        xb[t] = f.stage[t];
+        const double diff = xv[t] - xb[t];
+        wv[t] = wv[t] + rv[t] * diff;
+        if (live) PHX_OUT(const_cast<double*>(io.W)[(int64_t)t * S + sc], wv[t]);
+        dl += fabs(diff);
+    }
+    bool still = false, rework = false;
+    double xn[NS];                      // the certified lane's unscaled nonant x
+    if (live) {
+        ASet<PT> a;
+        aset_from_words<PT>(aw, a);
+        double xp[PT::NMAX_N], z[PT::NMAX_M];
+        PHX_UNROLL for (int j = 0; j < PT::n(); ++j) xp[j] = 0.0;
+        PHX_UNROLL for (int i = 0; i < PT::m(); ++i) z[i] = 0.0;
+        const Data<PT> D0(io, sc, av, wv, rv, xb);
+        const int c = io.warm_rounds > 0 ? as_round<PT>(io, D0, a, xp, z, 0) : 2;
+        if (c == 0) {
+            write_certified<PT>(io, D0, sc, a, xp, z, 0);
+            PHX_UNROLL for (int j = 0; j < PT::n(); ++j)
+                if (PT::col_slot(j) >= 0) xn[PT::col_slot(j)] = xp[j] * (PT::scaled() ? PT::dcs(j) : 1.0);
+        } else if (c == 1 && io.warm_rounds > 1) {
+            // round 1 onwards in the group's finisher: the state to go on from
+            rework = true;
+            PHX_UNROLL for (int j = 0; j < PT::n(); ++j) store_wt(&f.rx[(int64_t)j * S + sc], xp[j]);
+            PHX_UNROLL for (int i = 0; i < PT::m(); ++i) store_wt(&f.rz[(int64_t)i * S + sc], z[i]);
+            aset_store<PT>(io, sc, a);
+        } else {
+            if (c == 2) PHX_LANE_STAT(3);
+            aset_store<PT>(io, sc, a);   // the updated active set seeds the next pass
+            io.status[sc] = 0;
+            io.flags[sc] = 0;
+            still = true;
+        }
+    }
+    double v[NV];
+    PHX_UNROLL for (int e = 0; e < NV; ++e) v[e] = 0.0;
+    if (live) {
+        v[2 * NS] = dl;
+        if (!still && !rework)
+            PHX_UNROLL for (int t = 0; t < PT::nslot(); ++t) {
+                const double w = pcv[t] * xn[t];
+                v[t] += w;
+                v[NS + t] += w * xn[t];
+            }
+    }
+    compact_lane(still, sc, io.lanes_out, io.count_out);
+    const unsigned long long rm = __ballot(rework);
+    if (threadIdx.x == 0) store_wt_u64(&f.rmask[blockIdx.x], rm);
+    fz_fold_c<PT>(io, v);
 }
 
 #endif
