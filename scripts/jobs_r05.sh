@@ -14,7 +14,7 @@ case "$1" in
   s1)  # the whole GPU suite, then the driver's default command (compact line)
        $J "test:tests" && $J "bench:r05_s1_default:--detail gpurun_out/r05_s1_default_detail.json" ;;
   s2)  # the compacting fused kernel: parity, then headline / per-rank slice / 1M against PHX_FZC=0 (same box)
-       $J "test:tests/test_gpu_parity.py tests/test_trajectories.py" "bench:r05_s2_bench:$H" "bench:r05_s2_c3s8:$S8" \
+       $J "test:tests/test_gpu_parity.py tests/test_trajectories.py tests/test_bench_settings.py" "bench:r05_s2_bench:$H" "bench:r05_s2_c3s8:$S8" \
           "bench:r05_s2_1m:$M" && \
        PHX_FZC=0 $J "bench:r05_s2_bench_fz1:$H" "bench:r05_s2_c3s8_fz1:$S8" "bench:r05_s2_1m_fz1:$M" && \
        $J "prof:r05_s2_prof:$H --ar-probe 0" ;;

@@ -1,0 +1,85 @@
+"""The solver settings bench.py times, pinned by oracle comparisons (verdict r4,
+item 7): bench.py runs C2 (farmer crops_multiplier=10 x 1,000) with the
+workgroup pass's round budget wg_warm = 8 and C5a (sslp_15_45) with wg_warm = 4
+(bench.py workloads()); the default 16 is what the other parity tests use.
+Both run through the device loop (phx_iterk, workgroup mode: the budget decides
+which lanes stop the pipeline for the sparse solver).
+
+* C2: the full 1,000-scenario W / x-bar trajectory from the engine's Iter0
+  point against the oracle's PH iterations (phbase.py:27-107, 293-343,
+  875-979), as test_gpu_parity.test_farmer_cm10_1000_workgroup_gpu.
+* C5a: the 256-scenario sslp trajectory against the oracle golden
+  (tests/golden/traj_sslp_256.npz), as test_trajectories, and the full 10,000
+  scenarios with sampled oracle re-solves, as test_sslp.test_sslp_10k_gpu."""
+import pytest
+
+from helpers import all_certified, oracle_continue_from, rel, run_engine
+from mpisppy_amd.examples import farmer, sslp
+from oracle import models as om, ph as oph
+
+import bench
+
+
+def _bench_so(name):
+    so = bench.workloads()[name]["so"]
+    assert so == {"C2": {"wg_warm": 8}, "C5a": {"wg_warm": 4}}[name]   # the settings timed
+    return dict(so)
+
+
+def check_c2_bench_settings(lib, device, S=1000, it=5):
+    so = _bench_so("C2")
+    kw = {"num_scens": S, "crops_multiplier": 10}
+    scens = [om.farmer("scen%d" % k, crops_multiplier=10, num_scens=S) for k in range(S)]
+    opts = {"iter0_solver_options": dict(so), "iterk_solver_options": dict(so)}
+    ph = run_engine(farmer.scenario_creator, farmer.scenario_names_creator(S), kw, it, lib=lib, device=device,
+                    options=opts)[0]
+    assert hasattr(ph, "iterk_stats") and all_certified(ph)
+    ph0 = run_engine(farmer.scenario_creator, farmer.scenario_names_creator(S), kw, 0, lib=lib, device=device,
+                     options=opts)[0]
+    oc = oracle_continue_from(ph0, scens, it)
+    assert rel(ph.W_array(), oc.W) < 1e-6
+    assert rel(ph.xbar_by_node()["ROOT"][0], oc.xbar[0]) < 1e-8
+    assert rel(ph.nonant_values(), oc.xn()) < 1e-6
+    return ph
+
+
+def test_c2_bench_settings_emu(emu):
+    check_c2_bench_settings(emu, "cpu", S=40, it=3)
+
+
+@pytest.mark.gpu
+def test_c2_bench_settings_gpu(gpu_lib):
+    ph = check_c2_bench_settings(gpu_lib, None)
+    print("C2 wg_warm 8:", ph.iterk_stats)
+
+
+def check_c5a_bench_settings(lib, device):
+    import test_trajectories as tt
+    ph = tt.check_trajectory(lib, device, "sslp_256", solver=_bench_so("C5a"))
+    assert hasattr(ph, "iterk_stats")
+    return ph
+
+
+def test_c5a_bench_settings_emu(emu):
+    check_c5a_bench_settings(emu, "cpu")
+
+
+@pytest.mark.gpu
+def test_c5a_bench_settings_gpu(gpu_lib):
+    ph = check_c5a_bench_settings(gpu_lib, None)
+    print("C5a wg_warm 4 (256):", ph.iterk_stats)
+    # full size: every subproblem certified, sampled oracle re-solves
+    S, pick = 10000, [0, 1, 2, 4999, 5000, 9998, 9999]
+    so = _bench_so("C5a")
+    names = sslp.scenario_names_creator(S)
+    ph, conv, Eobj, tb = run_engine(sslp.scenario_creator, names, {"num_scens": S}, 3, lib=gpu_lib,
+                                    options={"iter0_solver_options": dict(so), "iterk_solver_options": dict(so)})
+    assert hasattr(ph, "iterk_stats") and all_certified(ph)
+    o = oph.OraclePH([om.sslp(names[k], num_scens=S) for k in pick], rho=1.0)
+    o.W = ph.W_array()[pick].copy()
+    import numpy as np
+    o.xbar = np.tile(ph.xbar_by_node()["ROOT"][0], (len(pick), 1))
+    o.W_on, o.prox_on = 1, 1
+    o.solve_loop()
+    assert rel(ph.nonant_values()[pick], o.xn()) < 1e-6
+    assert rel(ph._host("obj")[pick], o.obj) < 1e-8
