@@ -2279,18 +2279,22 @@ __device__ void fz_rework_group(const LaneIO& io, int g, double* gacc) {
         if (sc >= 0) {
             double av[NVA], wv[NS], rv[NS], xb[NS], pcv[NS];
             uint32_t aw[NW];
+            // (what other blocks of this launch wrote -- W, the active set, the
+            // stash -- is read with `sc1` loads: valid with the acquire above
+            // and without it, PHX_RELAXED_HANDOFF; the rest is launch-constant)
             PHX_UNROLL for (int k = 0; k < PT::nvar(); ++k) av[k] = io.Av[(int64_t)k * S + sc];
-            PHX_UNROLL for (int k = 0; k < aset_words(PT::n(), PT::m()); ++k) aw[k] = io.aset[(int64_t)k * S + sc];
+            PHX_UNROLL for (int k = 0; k < aset_words(PT::n(), PT::m()); ++k)
+                aw[k] = __hip_atomic_load(io.aset + (int64_t)k * S + sc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             PHX_UNROLL for (int t = 0; t < PT::nslot(); ++t) {
                 const int64_t o = (int64_t)t * S + sc;
-                wv[t] = io.W[o];
+                wv[t] = load_wt(io.W + o);
                 rv[t] = io.rho[o];
                 pcv[t] = f.pc[o];
                 xb[t] = f.stage[t];
             }
             double xp[PT::NMAX_N], z[PT::NMAX_M];
-            PHX_UNROLL for (int j = 0; j < PT::n(); ++j) xp[j] = f.rx[(int64_t)j * S + sc];
-            PHX_UNROLL for (int i = 0; i < PT::m(); ++i) z[i] = f.rz[(int64_t)i * S + sc];
+            PHX_UNROLL for (int j = 0; j < PT::n(); ++j) xp[j] = load_wt(f.rx + (int64_t)j * S + sc);
+            PHX_UNROLL for (int i = 0; i < PT::m(); ++i) z[i] = load_wt(f.rz + (int64_t)i * S + sc);
             ASet<PT> a;
             aset_from_words<PT>(aw, a);
             const Data<PT> D(io, sc, av, wv, rv, xb);

@@ -353,7 +353,10 @@ class SPBase:
 
     # ------------------------------------------------------------ device
     def _t(self, a, dtype):
-        return torch.as_tensor(np.ascontiguousarray(a), dtype=dtype).to(self.device)
+        a = np.ascontiguousarray(a)
+        if not a.flags.writeable:          # (the read-only probabilities: torch wants a writable buffer)
+            a = a.copy()
+        return torch.as_tensor(a, dtype=dtype).to(self.device)
 
     def _upload_batch(self):
         b = self.batch
