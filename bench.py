@@ -441,8 +441,8 @@ def dominant_kernel(ph, K, fused):
                 # (the one-wave build at every size unless PHX_FZ2=1, phx_kernels.hip)
                 fz2 = os.environ.get("PHX_FZ2") == "1"
                 kname = "phx_lane_warm_fz" if (fz2 and not small) else "phx_lane_warm_fz1"
-                # (the compacting build, phx_kernels.hip, unless PHX_FZC=0 / PHX_FZ_LEGACY=1)
-                if os.environ.get("PHX_FZC") != "0" and os.environ.get("PHX_FZ_LEGACY") != "1":
+                # (the compacting build, phx_kernels.hip, opt-in PHX_FZC=1)
+                if os.environ.get("PHX_FZC") == "1" and os.environ.get("PHX_FZ_LEGACY") != "1":
                     kname = "phx_lane_warm_fzc"
             else:
                 kname = "phx_lane_all" if small else "phx_lane_warm"

@@ -18,5 +18,11 @@ case "$1" in
           "bench:r05_s2_1m:$M" && \
        PHX_FZC=0 $J "bench:r05_s2_bench_fz1:$H" "bench:r05_s2_c3s8_fz1:$S8" "bench:r05_s2_1m_fz1:$M" && \
        $J "prof:r05_s2_prof:$H --ar-probe 0" ;;
+  s3)  # the workgroup / sparse solvers after the XCD-aware block remap: time, kernel trace, HBM bytes
+       $J "bench:r05_s3_c2:--only C2 $A" "bench:r05_s3_c5a:--only C5a $A" "bench:r05_s3_c5b:--only C5b $A" \
+          "prof:r05_s3_c2_prof:--only C2 $A" "prof:r05_s3_c5a_prof:--only C5a $A" \
+          "pmc:r05_pmc_c2_fetch:FETCH_SIZE:--only C2 $A" "pmc:r05_pmc_c2_write:WRITE_SIZE:--only C2 $A" \
+          "pmc:r05_pmc_c5a_fetch:FETCH_SIZE:--only C5a $A" "pmc:r05_pmc_c5a_write:WRITE_SIZE:--only C5a $A" \
+          "pmc:r05_pmc_c5b_fetch:FETCH_SIZE:--only C5b $A" "pmc:r05_pmc_c5b_write:WRITE_SIZE:--only C5b $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
