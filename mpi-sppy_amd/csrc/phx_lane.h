@@ -2160,7 +2160,14 @@ __device__ void warm_fused(const LaneIO& io) {
         if (REG) {
             const Data<PT> D0(io, sc, av, wv, rv, xb);
             c = io.warm_rounds > 0 ? as_round<PT>(io, D0, a, xp, z, 0) : 2;
-            PHX_NOUNROLL for (int r = 1; r < io.warm_rounds && c == 1; ++r) c = as_round<PT>(io, D0, a, xp, z, r);
+            int nr = 1;
+            PHX_NOUNROLL for (int r = 1; r < io.warm_rounds && c == 1; ++r, ++nr) c = as_round<PT>(io, D0, a, xp, z, r);
+            // (diagnostics: the wavefront's most rounds, PHX_LANE_STAMPS=1)
+            if (io.stamps) {
+                int wmax = 0;
+                for (int q = 1; q <= 8; ++q) wmax = __ballot(nr >= q) ? q : wmax;
+                if (threadIdx.x == 0) io.stamps[(uint64_t)blockIdx.x * 8 + 6] = (uint64_t)wmax;
+            }
             if (c == 2) PHX_LANE_STAT(3);
             if (c == 0) write_certified<PT>(io, D0, sc, a, xp, z, 0);
         } else {

@@ -24,5 +24,8 @@ case "$1" in
           "pmc:r05_pmc_c2_fetch:FETCH_SIZE:--only C2 $A" "pmc:r05_pmc_c2_write:WRITE_SIZE:--only C2 $A" \
           "pmc:r05_pmc_c5a_fetch:FETCH_SIZE:--only C5a $A" "pmc:r05_pmc_c5a_write:WRITE_SIZE:--only C5a $A" \
           "pmc:r05_pmc_c5b_fetch:FETCH_SIZE:--only C5b $A" "pmc:r05_pmc_c5b_write:WRITE_SIZE:--only C5b $A" ;;
+  s4)  # where a fused wave's time goes: phase stamps by most rounds; the clock under load (GRBM)
+       PHX_LANE_STAMPS=1 $J "bench:r05_s4_stamps:$H --ar-probe 0" "bench:r05_s4_c3s8_stamps:$S8" "bench:r05_s4_1m_stamps:$M" && \
+       $J "pmc:r05_s4_grbm:GRBM_GUI_ACTIVE,GRBM_COUNT:$H --ar-probe 0" "pmc:r05_s4_c3s8_grbm:GRBM_GUI_ACTIVE,GRBM_COUNT:$S8" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
