@@ -27,5 +27,9 @@ case "$1" in
   s4)  # where a fused wave's time goes: phase stamps by most rounds; the clock under load (GRBM)
        PHX_LANE_STAMPS=1 $J "bench:r05_s4_stamps:$H --ar-probe 0" "bench:r05_s4_c3s8_stamps:$S8" "bench:r05_s4_1m_stamps:$M" && \
        $J "pmc:r05_s4_grbm:GRBM_GUI_ACTIVE,GRBM_COUNT:$H --ar-probe 0" "pmc:r05_s4_c3s8_grbm:GRBM_GUI_ACTIVE,GRBM_COUNT:$S8" ;;
+  s5)  # two waves per SIMD with register-resident rounds (PHX_FZR2=1) against the one-wave build, same box
+       $J "bench:r05_s5_bench:$H" "bench:r05_s5_1m:$M" && \
+       PHX_FZR2=1 $J "bench:r05_s5_bench_r2:$H" "bench:r05_s5_1m_r2:$M" && \
+       PHX_FZR2=1 PHX_LANE_STAMPS=1 $J "bench:r05_s5_stamps_r2:$H --ar-probe 0" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
