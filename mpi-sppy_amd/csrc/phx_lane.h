@@ -210,11 +210,6 @@ struct LaneIO {
     double* map;           // [map_words<PT>()][S] affine solution maps (see map_apply), or null
     FusedW fz;             // phx_iterk fused Update_W (fz.on = 0 otherwise)
     uint64_t* stamps;      // diagnostics (PHX_LANE_STAMPS=1): [block][8] wall-clock phase stamps, or null
-    // the Schur factor cache (kkt_solve_kc): per lane the packed factor of the
-    // last factorised active set and the prox weights it was built with
-    // [kfac_words][S], and that active set's words [aset_words][S]; or null
-    double* kfac;
-    uint32_t* kfac_w;
 };
 
 // Phase stamps of phx_lane_warm (lane 0 of each wavefront; 100 MHz wall clock):
@@ -897,11 +892,10 @@ PHX_LD void aset_from_words(const uint32_t* w, ASet<PT>& a) {
     a.l = lw;
 }
 
-// An active set's words (2 bits per column / row: 0 free / inactive, 1 lower,
-// 2 upper; 3 never occurs)
 template <class PT>
-PHX_LD void aset_pack(const ASet<PT>& a, uint32_t* w) {
+PHX_LD void aset_store(const LaneIO& io, int sc, const ASet<PT>& a) {
     constexpr int NW = aset_words(PT::NMAX_N, PT::NMAX_M);
+    uint32_t w[NW];
     PHX_UNROLL for (int k = 0; k < NW; ++k) w[k] = 0u;
     PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
         const uint32_t v = a.F(j) ? 0u : (a.up(j) ? 2u : 1u);
@@ -912,13 +906,6 @@ PHX_LD void aset_pack(const ASet<PT>& a, uint32_t* w) {
         const uint32_t v = a.R(i) ? (a.lo(i) ? 1u : 2u) : 0u;
         w[b >> 5] |= v << (b & 31);
     }
-}
-
-template <class PT>
-PHX_LD void aset_store(const LaneIO& io, int sc, const ASet<PT>& a) {
-    constexpr int NW = aset_words(PT::NMAX_N, PT::NMAX_M);
-    uint32_t w[NW];
-    aset_pack<PT>(a, w);
     // (the word addresses recomputed from an opaque index: kept from aset_load
     // across the solve they were spilled to scratch)
     const int so = opaque_index(sc);
@@ -1173,63 +1160,6 @@ PHX_LD bool kkt_solve(const Data<PT>& D, const ASet<PT>& a, double* xp, double* 
     return true;
 }
 
-// The Schur factor cache (LaneIO::kfac, fused iterations): the packed Cholesky
-// factor depends only on the active set, the lane's A values and the prox
-// weights p (and the constant regularisation), so a lane whose round starts
-// from the active set it last factorised with the same p -- every PH
-// iteration's round 0 after a certified solve: it starts from the certified
-// active set -- reuses it bit for bit and skips the Schur assembly and the
-// Cholesky.  Keyed by the active set's words and p (compared bitwise); entries
-// start invalid (all-ones words, which no active set packs to).  Small factors
-// only (at most 64 packed entries).
-template <class PT>
-PHX_LD constexpr int kfac_tt() { return PT::NMAX_M * (PT::NMAX_M + 1) / 2; }
-template <class PT>
-PHX_LD constexpr bool kfac_on() { return kfac_tt<PT>() <= 64; }
-template <class PT>
-PHX_LD constexpr int kfac_words() { return kfac_tt<PT>() + (PT::nslot() > 0 ? PT::nslot() : 1); }
-
-// kkt_solve with the cache: Mc the cached factor (a hit), else factorise and,
-// with kls (this lane's LDS slot, stride 64), park the fresh factor there --
-// committed to io.kfac with its key only when the lane certifies
-// (kfac_commit: stores inside the round loop kept ~130 more registers live)
-template <class PT>
-PHX_LD bool kkt_solve_kc(const Data<PT>& D, const ASet<PT>& a, double* xp, double* z, const double* Mc,
-                         double* kls) {
-    constexpr int TT = kfac_tt<PT>();
-    constexpr double reg = KKT_REG;
-    KFactor<PT> K;
-    const AMul<PT> am(a);
-    if (Mc) {
-        PHX_UNROLL for (int t = 0; t < TT; ++t) K.M[t] = Mc[t];
-        // (kkt_factor's expression)
-        PHX_UNROLL for (int j = 0; j < PT::n(); ++j)
-            if (PT::col_slot(j) >= 0) K.ipn[PT::col_slot(j)] = 1.0 / (D.p(j) + reg);
-    } else {
-        if (!kkt_factor<PT>(D, am, K)) return false;
-        if (kls) PHX_UNROLL for (int t = 0; t < TT; ++t) kls[t * 64] = K.M[t];
-    }
-    kkt_refine<PT>(D, am, K, RhsFull<PT>{D, a}, xp, z);
-    return true;
-}
-
-// A certified lane's fresh factor (parked in LDS by kkt_solve_kc) into the
-// cache, keyed by its active set and prox weights
-template <class PT>
-PHX_LD void kfac_commit(const LaneIO& io, int sc, const double* kls, const double* pn, const ASet<PT>& a) {
-    constexpr int TT = kfac_tt<PT>();
-    const int64_t S = io.S;
-    const int so = opaque_index(sc);
-    double* kf = io.kfac + so;
-    PHX_UNROLL for (int t = 0; t < TT; ++t) PHX_OUT(kf[(int64_t)t * S], kls[t * 64]);
-    PHX_UNROLL for (int t = 0; t < PT::nslot(); ++t) PHX_OUT(kf[(int64_t)(TT + t) * S], pn[t]);
-    uint32_t w[aset_words(PT::NMAX_N, PT::NMAX_M)];
-    aset_pack<PT>(a, w);
-    uint32_t* kwp = io.kfac_w + so;
-    PHX_UNROLL for (int k = 0; k < aset_words(PT::n(), PT::m()); ++k) PHX_OUT(kwp[(int64_t)k * S], w[k]);
-}
-
-
 // ---------------------------------------------------------------------------
 // Affine solution map of one active set.  With the active set and the prox
 // weights p fixed, the KKT solution is affine in the nonant linear terms qn:
@@ -1471,14 +1401,6 @@ template <class PT>
 PHX_LD int as_round(const LaneIO& io, const Data<PT>& D, ASet<PT>& a, double* xp, double* z, int r) {
     PHX_LANE_STAT(0);
     if (!kkt_solve<PT>(D, a, xp, z)) return 3;
-    return certify_update<PT>(D, a, xp, z, io.kkt_tol, r >= io.single_after);
-}
-// ... with the factor cache (kkt_solve_kc): Mc the cached factor of a, or null
-template <class PT>
-PHX_LD int as_round_kc(const LaneIO& io, const Data<PT>& D, ASet<PT>& a, double* xp, double* z, int r,
-                       const double* Mc, double* kls) {
-    PHX_LANE_STAT(0);
-    if (!kkt_solve_kc<PT>(D, a, xp, z, Mc, kls)) return 3;
     return certify_update<PT>(D, a, xp, z, io.kkt_tol, r >= io.single_after);
 }
 // r0: the index of the first round (the fused kernel runs round 0 itself)
@@ -2186,7 +2108,7 @@ __device__ __forceinline__ void compact_lane(bool still, int sc, int32_t* out, i
 // data in registers -- the other builds re-load it per round (kept live across
 // the round loop it spilled; a re-load is a memory round trip per round)
 template <class PT, bool REG = false>
-__device__ __forceinline__ void warm_fused(const LaneIO& io) {
+__device__ void warm_fused(const LaneIO& io) {
     const FusedW& f = io.fz;
     constexpr int NS = PT::nslot() > 0 ? PT::nslot() : 1;
     constexpr int NV = 2 * NS + 1;
@@ -2208,20 +2130,6 @@ __device__ __forceinline__ void warm_fused(const LaneIO& io) {
             rv[t] = io.rho[o];
             pcv[t] = f.pc[o];
         }
-    }
-    // the factor cache's entry (REG builds: round 0 reuses it when its key
-    // matches), loaded with the rest
-    constexpr int KT = kfac_on<PT>() ? kfac_words<PT>() : 1;
-    double kc[KT];
-    uint32_t kw[NW];
-    const bool kc_ld = REG && kfac_on<PT>() && io.kfac != nullptr;
-    // this lane's LDS slot for a fresh factor (stride 64: lane-contiguous rows)
-    __shared__ double kfs[(kfac_on<PT>() && REG ? kfac_tt<PT>() : 1) * 64];
-    double* kls = kfs + threadIdx.x;
-    uint32_t kc_new = 0u;
-    if (kc_ld) {
-        PHX_UNROLL for (int e = 0; e < kfac_words<PT>(); ++e) kc[e] = io.kfac[(int64_t)e * S + s];
-        PHX_UNROLL for (int k = 0; k < aset_words(PT::n(), PT::m()); ++k) kw[k] = io.kfac_w[(int64_t)k * S + s];
     }
     lane_stamp(io, 0);
     if (gated(io.gate)) return;
@@ -2251,31 +2159,9 @@ __device__ __forceinline__ void warm_fused(const LaneIO& io) {
         int c;
         if (REG) {
             const Data<PT> D0(io, sc, av, wv, rv, xb);
-            if (kc_ld) {
-                // a hit: the entry's active set is this round's and its p this iteration's
-                bool hit = true;
-                PHX_UNROLL for (int k = 0; k < aset_words(PT::n(), PT::m()); ++k) hit = hit && kw[k] == aw[k];
-                PHX_UNROLL for (int t = 0; t < PT::nslot(); ++t) hit = hit && kc[kfac_tt<PT>() + t] == D0.pn[t];
-                // (wave-uniform: a wavefront with a miss factorises in every lane --
-                // the same bits a hit would give -- so the cached factor and a fresh
-                // one are never live together)
-                const bool wave_hit = __ballot(!hit) == 0ull;
-                c = io.warm_rounds > 0 ? as_round_kc<PT>(io, D0, a, xp, z, 0, wave_hit ? kc : nullptr,
-                                                          wave_hit ? nullptr : kls)
-                                       : 2;
-                kc_new = wave_hit ? 0u : 1u;
-            } else {
-                c = io.warm_rounds > 0 ? as_round<PT>(io, D0, a, xp, z, 0) : 2;
-            }
+            c = io.warm_rounds > 0 ? as_round<PT>(io, D0, a, xp, z, 0) : 2;
             int nr = 1;
-            PHX_NOUNROLL for (int r = 1; r < io.warm_rounds && c == 1; ++r, ++nr) {
-                if (kc_ld) {
-                    c = as_round_kc<PT>(io, D0, a, xp, z, r, nullptr, kls);
-                    kc_new = 1u;
-                } else {
-                    c = as_round<PT>(io, D0, a, xp, z, r);
-                }
-            }
+            PHX_NOUNROLL for (int r = 1; r < io.warm_rounds && c == 1; ++r, ++nr) c = as_round<PT>(io, D0, a, xp, z, r);
             // (diagnostics: the wavefront's most rounds, PHX_LANE_STAMPS=1)
             if (io.stamps) {
                 int wmax = 0;
@@ -2284,7 +2170,6 @@ __device__ __forceinline__ void warm_fused(const LaneIO& io) {
             }
             if (c == 2) PHX_LANE_STAT(3);
             if (c == 0) write_certified<PT>(io, D0, sc, a, xp, z, 0);
-            if (c == 0 && kc_new) kfac_commit<PT>(io, sc, kls, D0.pn, a);
         } else {
             {
                 const Data<PT> D0(io, sc, av, wv, rv, xb);
@@ -2540,7 +2425,7 @@ __device__ void fz_fold_c(const LaneIO& io, double* v) {
 }
 
 template <class PT>
-__device__ __forceinline__ void warm_fused_c(const LaneIO& io) {
+__device__ void warm_fused_c(const LaneIO& io) {
     const FusedW& f = io.fz;
     constexpr int NS = PT::nslot() > 0 ? PT::nslot() : 1;
     constexpr int NV = 2 * NS + 1;

@@ -31,10 +31,5 @@ case "$1" in
        $J "bench:r05_s5_bench:$H" "bench:r05_s5_1m:$M" && \
        PHX_FZR2=1 $J "bench:r05_s5_bench_r2:$H" "bench:r05_s5_1m_r2:$M" && \
        PHX_FZR2=1 PHX_LANE_STAMPS=1 $J "bench:r05_s5_stamps_r2:$H --ar-probe 0" ;;
-  s6)  # the fused kernels' Schur factor cache: parity, then against PHX_KFAC=0 (same box)
-       $J "test:tests/test_gpu_parity.py tests/test_trajectories.py" "bench:r05_s6_bench:$H" "bench:r05_s6_c3s8:$S8" \
-          "bench:r05_s6_1m:$M" && \
-       PHX_KFAC=0 $J "bench:r05_s6_bench_nokc:$H" "bench:r05_s6_c3s8_nokc:$S8" "bench:r05_s6_1m_nokc:$M" && \
-       PHX_LANE_STAMPS=1 $J "bench:r05_s6_stamps:$H --ar-probe 0" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
