@@ -2108,7 +2108,7 @@ __device__ __forceinline__ void compact_lane(bool still, int sc, int32_t* out, i
 // data in registers -- the other builds re-load it per round (kept live across
 // the round loop it spilled; a re-load is a memory round trip per round)
 template <class PT, bool REG = false>
-__device__ void warm_fused(const LaneIO& io) {
+__device__ __forceinline__ void warm_fused(const LaneIO& io) {
     const FusedW& f = io.fz;
     constexpr int NS = PT::nslot() > 0 ? PT::nslot() : 1;
     constexpr int NV = 2 * NS + 1;
@@ -2425,7 +2425,7 @@ __device__ void fz_fold_c(const LaneIO& io, double* v) {
 }
 
 template <class PT>
-__device__ void warm_fused_c(const LaneIO& io) {
+__device__ __forceinline__ void warm_fused_c(const LaneIO& io) {
     const FusedW& f = io.fz;
     constexpr int NS = PT::nslot() > 0 ? PT::nslot() : 1;
     constexpr int NV = 2 * NS + 1;
