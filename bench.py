@@ -441,6 +441,9 @@ def dominant_kernel(ph, K, fused):
                 # (the one-wave build at every size unless PHX_FZ2=1, phx_kernels.hip)
                 fz2 = os.environ.get("PHX_FZ2") == "1"
                 kname = "phx_lane_warm_fz" if (fz2 and not small) else "phx_lane_warm_fz1"
+                # (above one wavefront per SIMD the two-wave build, unless PHX_FZR2=0)
+                if not small and not fz2 and os.environ.get("PHX_FZR2") != "0":
+                    kname = "phx_lane_warm_fzr2"
                 # (the compacting build, phx_kernels.hip, opt-in PHX_FZC=1)
                 if os.environ.get("PHX_FZC") == "1" and os.environ.get("PHX_FZ_LEGACY") != "1":
                     kname = "phx_lane_warm_fzc"
@@ -497,7 +500,7 @@ def roofline(kernel, avg_s, launches, bpu, units, traffic=None, traffic_src=None
 # how phx_iterk's events time the dominant kernel (bench --timing-every < 0)
 LAUNCH_TIMING = {k: ("one HIP event pair around all the fused launches of the timed loop (back to back on "
                      "phx_iterk's stream; no per-launch records in between)")
-                 for k in ("phx_lane_warm_fz", "phx_lane_warm_fz1", "phx_lane_warm_fzc")}
+                 for k in ("phx_lane_warm_fz", "phx_lane_warm_fz1", "phx_lane_warm_fzc", "phx_lane_warm_fzr2")}
 
 
 def run_config(name, w, args, K, so, world, dev):

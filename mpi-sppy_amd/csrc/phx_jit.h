@@ -300,8 +300,8 @@ inline std::string lane_kernel_source(const LaneStructure& L, int warm_waves = 1
          "  phx_lane::warm_fused<PT, true>(io);\n"
          "#endif\n"
          "}\n";
-    // ... two waves per SIMD with every round on register data (experiment,
-    // PHX_FZR2=1: the compiler spills what does not fit 256 registers)
+    // ... two waves per SIMD with every round on register data (above one
+    // wavefront per SIMD; the compiler spills what does not fit 256 registers)
     o << "extern \"C\" __global__ void __launch_bounds__(64, 2) phx_lane_warm_fzr2(phx_lane::LaneIO io) {\n"
          "  phx_lane::warm_fused<PT, true>(io);\n"
          "}\n";

@@ -31,5 +31,9 @@ case "$1" in
        $J "bench:r05_s5_bench:$H" "bench:r05_s5_1m:$M" && \
        PHX_FZR2=1 $J "bench:r05_s5_bench_r2:$H" "bench:r05_s5_1m_r2:$M" && \
        PHX_FZR2=1 PHX_LANE_STAMPS=1 $J "bench:r05_s5_stamps_r2:$H --ar-probe 0" ;;
+  s7)  # the two-wave build by default; post-solve values parked in LDS (JIT define), same box
+       $J "test:tests/test_gpu_parity.py -k fused" "bench:r05_s7_bench:$H" "bench:r05_s7_1m:$M" && \
+       PHX_LANE_DEFS=PHX_FZ_LDS_KEEP $J "bench:r05_s7_bench_keep:$H" "bench:r05_s7_1m_keep:$M" && \
+       $J "bench:r05_s7_bench_b:$H" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
