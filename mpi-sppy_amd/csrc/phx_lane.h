@@ -2146,7 +2146,7 @@ __device__ __forceinline__ void warm_fused(const LaneIO& io) {
         dl += fabs(diff);
     }
     lane_stamp(io, 2);
-#ifdef PHX_FZ_LDS_KEEP
+#ifndef PHX_FZ_NO_LDS_KEEP
     // (values needed only after the solve, parked in LDS across it)
     __shared__ double fz_keep[(NS + 1) * 64];
     PHX_UNROLL for (int t = 0; t < PT::nslot(); ++t) fz_keep[t * 64 + threadIdx.x] = pcv[t];
@@ -2202,7 +2202,7 @@ __device__ __forceinline__ void warm_fused(const LaneIO& io) {
     // its convergence term
     double v[NV];
     PHX_UNROLL for (int e = 0; e < NV; ++e) v[e] = 0.0;
-#ifdef PHX_FZ_LDS_KEEP
+#ifndef PHX_FZ_NO_LDS_KEEP
     PHX_UNROLL for (int t = 0; t < PT::nslot(); ++t) pcv[t] = fz_keep[t * 64 + threadIdx.x];
     dl = fz_keep[NS * 64 + threadIdx.x];
 #endif

@@ -35,5 +35,7 @@ case "$1" in
        $J "test:tests/test_gpu_parity.py -k fused" "bench:r05_s7_bench:$H" "bench:r05_s7_1m:$M" && \
        PHX_LANE_DEFS=PHX_FZ_LDS_KEEP $J "bench:r05_s7_bench_keep:$H" "bench:r05_s7_1m_keep:$M" && \
        $J "bench:r05_s7_bench_b:$H" ;;
+  s8)  # the headline's timed region on the GPU timeline (kernel trace + HIP API trace)
+       $J "prof:r05_s8_prof:$H --ar-probe 0" "trace:r05_s8_trace:$H --ar-probe 0" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
