@@ -37,5 +37,7 @@ case "$1" in
        $J "bench:r05_s7_bench_b:$H" ;;
   s8)  # the headline's timed region on the GPU timeline (kernel trace + HIP API trace)
        $J "prof:r05_s8_prof:$H --ar-probe 0" "trace:r05_s8_trace:$H --ar-probe 0" ;;
+  s9)  # the host's share of the timed region (wall stamps + cProfile)
+       $J "py:r05_s9_cprof:scripts/timed_cprof.py" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
