@@ -39,5 +39,11 @@ case "$1" in
        $J "prof:r05_s8_prof:$H --ar-probe 0" "trace:r05_s8_trace:$H --ar-probe 0" ;;
   s9)  # the host's share of the timed region (wall stamps + cProfile)
        $J "py:r05_s9_cprof:scripts/timed_cprof.py" ;;
+  s10) # the host's timed-region call tree (every PHBase/SPOpt/SPBase method and ABI call)
+       $J "py:r05_s10_wall:scripts/iter0_wall.py" ;;
+  s11) # Iter0's interior point at two waves per SIMD (PHX_COLD_WAVES=2, spills) against one, same box
+       $J "bench:r05_s11_bench:$H --ar-probe 0" "bench:r05_s11_1m:$M" && \
+       PHX_COLD_WAVES=2 $J "bench:r05_s11_bench_cw2:$H --ar-probe 0" "bench:r05_s11_1m_cw2:$M" \
+          "prof:r05_s11_prof_cw2:$H --ar-probe 0" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
