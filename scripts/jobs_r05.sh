@@ -45,5 +45,7 @@ case "$1" in
        $J "bench:r05_s11_bench:$H --ar-probe 0" "bench:r05_s11_1m:$M" && \
        PHX_COLD_WAVES=2 $J "bench:r05_s11_bench_cw2:$H --ar-probe 0" "bench:r05_s11_1m_cw2:$M" \
           "prof:r05_s11_prof_cw2:$H --ar-probe 0" ;;
+  s12) # the workgroup solver's phase clocks in the device loop (C2, C5a)
+       PHX_WG_PROF=1 $J "bench:r05_s12_c2_wgprof:--only C2 $A" "bench:r05_s12_c5a_wgprof:--only C5a $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
