@@ -47,5 +47,9 @@ case "$1" in
           "prof:r05_s11_prof_cw2:$H --ar-probe 0" ;;
   s12) # the workgroup solver's phase clocks in the device loop (C2, C5a)
        PHX_WG_PROF=1 $J "bench:r05_s12_c2_wgprof:--only C2 $A" "bench:r05_s12_c5a_wgprof:--only C5a $A" ;;
+  s13) # the workgroup mode's in-stream sparse step: parity (workgroup / sparse / trajectories), C2 / C5a against the stop (same box)
+       $J "test:tests/test_gpu_parity.py tests/test_trajectories.py tests/test_bench_settings.py tests/test_sslp.py" \
+          "bench:r05_s13_c2:--only C2 $A" "bench:r05_s13_c5a:--only C5a $A" && \
+       PHX_WG_SP_INLINE=0 $J "bench:r05_s13_c2_stop:--only C2 $A" "bench:r05_s13_c5a_stop:--only C5a $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
