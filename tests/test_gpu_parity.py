@@ -419,12 +419,18 @@ def test_native_loop_workgroup_matches_host_loop_gpu(gpu_lib):
     assert a.iterk_stats["not_optimal"] == 0
 
 
-def test_native_loop_workgroup_stragglers_gpu(gpu_lib):
-    """One workgroup round per solve: uncertified lanes stop the device loop,
-    which finishes them with PDHG + polish and resumes; same trajectory."""
+@pytest.mark.parametrize("sp", [1, 0])
+def test_native_loop_workgroup_stragglers_gpu(gpu_lib, sp):
+    """One workgroup round per solve: the lanes it leaves go on to the sparse
+    solver's interior point in the stream (sp 1: no pipeline stop), or without
+    the sparse solver (sp 0) stop the device loop, which finishes them with PDHG
+    + polish and resumes; either way the host loop's trajectory, bit for bit."""
     from test_engine_emu import check_native_vs_host_wg
-    a, b = check_native_vs_host_wg(gpu_lib, None, S=300, iters=5, solver={"wg_warm": 1})
-    assert a.iterk_stats["straggler_stops"] > 0
+    a, b = check_native_vs_host_wg(gpu_lib, None, S=300, iters=5, solver={"wg_warm": 1, "sp": sp})
+    if sp:
+        assert a.iterk_stats["straggler_stops"] == 0
+    else:
+        assert a.iterk_stats["straggler_stops"] > 0
 
 
 @pytest.mark.parametrize("fused", [0, 1])
