@@ -267,13 +267,14 @@ def test_time_to_conv_emu(emu):
     assert ph._PHIter == 94
 
 
-def check_native_vs_host_wg(lib, device, S=20, iters=5, solver=None):
+def check_native_vs_host_wg(lib, device, S=20, iters=5, solver=None, iterk_extra=None):
     """Subproblems above the lane solver's limits (farmer crops_multiplier=10):
     phx_iterk runs the workgroup warm pass per iteration (stragglers through
-    the stop / finish / resume protocol) == the host loop, bit for bit."""
+    the stop / finish / resume protocol) == the host loop, bit for bit.
+    iterk_extra: solver options of the PH iterations only."""
     runs = []
     for nl in (1, 0):
-        so = dict(solver or {}, native_loop=nl)
+        so = dict(solver or {}, native_loop=nl, **(iterk_extra or {}))
         opts = {"iter0_solver_options": dict(solver or {}), "iterk_solver_options": so}
         runs.append(run_engine(farmer.scenario_creator, farmer.scenario_names_creator(S),
                                {"num_scens": S, "crops_multiplier": 10}, iters, lib=lib, device=device,

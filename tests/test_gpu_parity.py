@@ -419,18 +419,30 @@ def test_native_loop_workgroup_matches_host_loop_gpu(gpu_lib):
     assert a.iterk_stats["not_optimal"] == 0
 
 
-@pytest.mark.parametrize("sp", [1, 0])
-def test_native_loop_workgroup_stragglers_gpu(gpu_lib, sp):
+@pytest.mark.parametrize("ipm_cut", [0, 1])
+def test_native_loop_workgroup_stragglers_gpu(gpu_lib, ipm_cut):
     """One workgroup round per solve: the lanes it leaves go on to the sparse
-    solver's interior point in the stream (sp 1: no pipeline stop), or without
-    the sparse solver (sp 0) stop the device loop, which finishes them with PDHG
-    + polish and resumes; either way the host loop's trajectory, bit for bit."""
+    solver's interior point in the stream (no pipeline stop); with that interior
+    point cut to 2 iterations (ipm_cut) its leftovers stop the device loop,
+    which finishes them with PDHG + polish and resumes.  Either way the host
+    loop's trajectory, bit for bit."""
     from test_engine_emu import check_native_vs_host_wg
-    a, b = check_native_vs_host_wg(gpu_lib, None, S=300, iters=5, solver={"wg_warm": 1, "sp": sp})
-    if sp:
-        assert a.iterk_stats["straggler_stops"] == 0
-    else:
+    a, b = check_native_vs_host_wg(gpu_lib, None, S=300, iters=5, solver={"wg_warm": 1},
+                                   iterk_extra={"ipm_max_it": 2} if ipm_cut else None)
+    if ipm_cut:
         assert a.iterk_stats["straggler_stops"] > 0
+    else:
+        assert a.iterk_stats["straggler_stops"] == 0
+
+
+def test_sp_off_on_sparse_context_raises_gpu(gpu_lib):
+    """sp = 0 (the dense generic path) on a context that holds the sparse
+    solver's workspaces only: refused with an error, not run on absent buffers."""
+    from mpisppy_amd._native import NativeError
+    so = {"wg_warm": 1, "sp": 0}
+    with pytest.raises(NativeError, match="sp = 0"):
+        run_engine(farmer.scenario_creator, farmer.scenario_names_creator(30), {"num_scens": 30, "crops_multiplier": 10},
+                   2, lib=gpu_lib, options={"iter0_solver_options": dict(so), "iterk_solver_options": dict(so)})
 
 
 @pytest.mark.parametrize("fused", [0, 1])
