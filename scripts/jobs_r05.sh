@@ -51,5 +51,7 @@ case "$1" in
        $J "test:tests/test_gpu_parity.py tests/test_trajectories.py tests/test_bench_settings.py tests/test_sslp.py" \
           "bench:r05_s13_c2:--only C2 $A" "bench:r05_s13_c5a:--only C5a $A" && \
        PHX_WG_SP_INLINE=0 $J "bench:r05_s13_c2_stop:--only C2 $A" "bench:r05_s13_c5a_stop:--only C5a $A" ;;
+  s14) # C4 (aircond 10x10x10): kernel trace of the timed iterations
+       $J "prof:r05_s14_c4_prof:--only C4 $A" "bench:r05_s14_c4:--only C4 $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
