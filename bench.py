@@ -302,10 +302,13 @@ def workloads():
                    kw=lambda S, cm: {"num_scens": 1000, "crops_multiplier": 10}, nodes=None, S=1000,
                    desc="farmer crops_multiplier=10, 1,000 scenarios (BASELINE configs[1])",
                    # the workgroup pass's round budget: the lanes that need more
-                   # stop the loop for the sparse interior point either way
-                   # (measured, r04_s31/s32: 16 rounds 0.98-0.99 ms per step, 8
-                   # 0.94-0.95, 6 0.92, 4 2.76 -- eight stops instead of one)
-                   so={"wg_warm": 8},
+                   # go on to the sparse interior point either way (measured,
+                   # r04_s31/s32: 16 rounds 0.98-0.99 ms per step, 8 0.94-0.95,
+                   # 6 0.92, 4 2.76 -- eight stops instead of one); in the first
+                   # PH iteration after Iter0 the pass certifies almost no lane
+                   # (emulation, 300 scenarios: 12 of 300 with 8 rounds), so one
+                   # round there (wg_first) before the interior point
+                   so={"wg_warm": 8, "wg_first": 1},
                    cpu=dict(model="farmer", cm=10, scens=1000, iters=2, total=1000)),
         "C4": dict(creator=aircond.scenario_creator, names=lambda S: ["scen%d" % i for i in range(1000)],
                    kw=lambda S, cm: {"branching_factors": bfs}, S=1000,

@@ -123,6 +123,12 @@ typedef struct phx_solve_opts {
                                  expose the active set (classification, then
                                  active-set rounds certify to kkt_tol);
                                  0: ipm_tol                                   */
+    int32_t wg_first;         /* k > 0: the workgroup pass of the first warm
+                                 solve after a cold one (the first PH iteration
+                                 after Iter0) runs at most k rounds instead of
+                                 wg_warm -- where that solve's active sets move
+                                 too far for the pass and the sparse solver's
+                                 interior point takes most lanes anyway; 0: wg_warm */
 } phx_solve_opts;
 
 /* Statistics of the most recent phx_solve (HIP events on the solve stream). */

@@ -43,6 +43,7 @@ class SolveOpts(ctypes.Structure):
         ("lane_solver", c_int32), ("as_rounds", c_int32), ("warm_passes", c_int32),
         ("defer", c_int32), ("wg_warm", c_int32), ("sp", c_int32), ("sp_rounds", c_int32),
         ("seed_templates", c_int32), ("rescue_rounds", c_int32), ("lane_ipm_tol", c_double),
+        ("wg_first", c_int32),
     ]
 
 

@@ -13,7 +13,7 @@ passes solver options (``iter0_solver_options`` / ``iterk_solver_options``,
 phbase.py:273-275): keys ``pdhg_max_iters``, ``pdhg_check_every``,
 ``pdhg_restart_max``, ``polish``, ``polish_refine``, ``polish_below``,
 ``kkt_tol``, ``opt_tol``, ``polish_reg``, ``warm_start``, ``ipm_after``,
-``ipm_max_it``, ``ipm_tol``, ``lane_solver``, ``as_rounds``, ``warm_passes``, ``wg_warm``,
+``ipm_max_it``, ``ipm_tol``, ``lane_solver``, ``as_rounds``, ``warm_passes``, ``wg_warm``, ``wg_first``,
 ``sp``, ``sp_rounds``, ``seed_templates``, ``rescue_rounds``, ``lane_ipm_tol``.
 """
 import ctypes
@@ -50,6 +50,7 @@ SOLVER_DEFAULTS = {
     "seed_templates": 64,
     "rescue_rounds": 0,
     "lane_ipm_tol": 0.0,
+    "wg_first": 0,
 }
 
 OPTIMAL, ITER_LIMIT, NUMERIC_FAIL, INFEASIBLE = 1, 2, 3, 4
@@ -158,6 +159,7 @@ class SPOpt(SPBase):
         so.seed_templates = int(o["seed_templates"])
         so.rescue_rounds = int(o["rescue_rounds"])
         so.lane_ipm_tol = float(o["lane_ipm_tol"])
+        so.wg_first = int(o["wg_first"])
         return so
 
     def _set_ph_terms(self):

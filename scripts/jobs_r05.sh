@@ -53,5 +53,8 @@ case "$1" in
        PHX_WG_SP_INLINE=0 $J "bench:r05_s13_c2_stop:--only C2 $A" "bench:r05_s13_c5a_stop:--only C5a $A" ;;
   s14) # C4 (aircond 10x10x10): kernel trace of the timed iterations
        $J "prof:r05_s14_c4_prof:--only C4 $A" "bench:r05_s14_c4:--only C4 $A" ;;
+  s15) # C2 with one workgroup round in the first PH iteration (wg_first) against eight, same box
+       $J "test:tests/test_bench_settings.py tests/test_gpu_parity.py -k workgroup" \
+          "bench:r05_s15_c2:--only C2 $A" "bench:r05_s15_c2_wf0:--only C2 $A --so {\"wg_first\":0}" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
