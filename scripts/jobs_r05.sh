@@ -56,5 +56,7 @@ case "$1" in
   s15) # C2 with one workgroup round in the first PH iteration (wg_first) against eight, same box
        $J "test:tests/test_bench_settings.py tests/test_gpu_parity.py -k workgroup" \
           "bench:r05_s15_c2:--only C2 $A" "bench:r05_s15_c2_wf0:--only C2 $A --so {\"wg_first\":0}" ;;
+  s16) # the whole GPU suite, then the driver's default command
+       $J "test:tests" && $J "bench:r05_s16_default:--detail gpurun_out/r05_s16_default_detail.json" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
