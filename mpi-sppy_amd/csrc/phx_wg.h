@@ -78,6 +78,12 @@ struct WgPairs {
     int32_t N;
     char* split;          // [S][split_stride] wg_carve's split arrays, or null (all in LDS)
     int64_t split_stride;
+    // the split layout's scenario-invariant parts, shared by every workgroup
+    // instead of copied into each scenario's area (null: copied): the CSC row
+    // indices / CSR positions as 16-bit, and A's values when no entry varies
+    const int16_t* pat_ri = nullptr;
+    const int16_t* pat_c2 = nullptr;
+    const double* a_const = nullptr;
     int32_t single_after = WG_SINGLE_AFTER;   // rounds of full primal-dual changes before single ones
 };
 
@@ -91,15 +97,20 @@ struct WgLds {
     int16_t *ar, *pos;                 // active rows (compact order) and each row's position (-1: inactive)
     int32_t* flag;
     int8_t *cc, *rc;   // column code 0 free / 1 at l / 2 at u; row code 0 inactive / 1 at bl / 2 at bu
+    bool own_a, own_pat;   // a / (ri, c2) are this scenario's copies (else the shared arrays)
 };
 
 // Split layout (split = true): the scenario's A values, the column vectors
 // (xp, r1, qq, pp) and the CSC row / position indices (ri, c2) live in a
 // per-scenario global scratch area (wg_split_bytes) instead of LDS, so that
 // more workgroups fit a CU (sslp_15_45: 75 KB of LDS, two per CU, against
-// 37 KB, four).
-PHX_HD size_t wg_split_bytes(int n, int nnz) {
-    return (8 * ((size_t)nnz + 4 * (size_t)n) + 4 * (size_t)nnz + 15) & ~(size_t)15;
+// 37 KB, four).  Round 5: the indices (always) and A's values (when none
+// varies: sslp) are read from arrays shared by every workgroup (WgPairs
+// pat_ri / pat_c2 / a_const, L2-resident) instead -- the per-scenario area
+// holds the four column vectors only (sslp: 39 -> 23 KB written and re-read
+// per scenario).
+PHX_HD size_t wg_split_bytes(int n, int nnz, bool own_a = true, bool own_pat = true) {
+    return (8 * ((own_a ? (size_t)nnz : 0) + 4 * (size_t)n) + (own_pat ? 4 * (size_t)nnz : 0) + 15) & ~(size_t)15;
 }
 
 PHX_HD size_t wg_lds_bytes(int n, int m, int nnz, bool split = false) {
@@ -110,9 +121,13 @@ PHX_HD size_t wg_lds_bytes(int n, int m, int nnz, bool split = false) {
     return (b + 15) & ~(size_t)15;
 }
 
-// gbase: the split arrays' place (null: everything in LDS)
-PHX_HD WgLds wg_carve(void* base, int n, int m, int nnz, void* gbase = nullptr) {
+// gbase: the split arrays' place (null: everything in LDS); with it, the
+// shared index arrays (ri_sh, c2_sh) and A values (a_sh) when given
+PHX_HD WgLds wg_carve(void* base, int n, int m, int nnz, void* gbase = nullptr, const int16_t* ri_sh = nullptr,
+                      const int16_t* c2_sh = nullptr, const double* a_sh = nullptr) {
     WgLds L;
+    L.own_a = !(gbase && a_sh);
+    L.own_pat = !(gbase && ri_sh && c2_sh);
     double* d = (double*)base;
     L.Sm = d; d += (size_t)m * (m + 1);   // rows padded to an odd stride (wg_warm)
     L.dg = d; d += m;
@@ -120,7 +135,8 @@ PHX_HD WgLds wg_carve(void* base, int n, int m, int nnz, void* gbase = nullptr) 
     L.t = d; d += m;
     L.u = d; d += m;
     double* g = gbase ? (double*)gbase : d;
-    L.a = g; g += nnz;
+    if (L.own_a) { L.a = g; g += nnz; }
+    else L.a = (double*)a_sh;          // (never written: own_a)
     L.xp = g; g += n;
     L.r1 = g; g += n;
     L.qq = g; g += n;
@@ -131,7 +147,8 @@ PHX_HD WgLds wg_carve(void* base, int n, int m, int nnz, void* gbase = nullptr) 
     int16_t* w = (int16_t*)(L.flag + 4);
     int16_t* gw = gbase ? (int16_t*)g : nullptr;
     L.cp = w; w += n + 1;
-    if (gw) { L.ri = gw; gw += nnz; L.c2 = gw; gw += nnz; }
+    if (!L.own_pat) { L.ri = (int16_t*)ri_sh; L.c2 = (int16_t*)c2_sh; }   // (never written)
+    else if (gw) { L.ri = gw; gw += nnz; L.c2 = gw; gw += nnz; }
     else { L.ri = w; w += nnz; L.c2 = w; w += nnz; }
     L.rp = w; w += m + 1;
     L.ci = w; w += nnz;
@@ -559,9 +576,11 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
     const double reg = O.reg;
     // ---- scenario data and the pattern into LDS ----
     for (int k = WG_TID; k < P.nnz; k += WG_NT) {
-        L.a[k] = aval(P, k, s);
-        L.ri[k] = (int16_t)P.rowidx[k];
-        L.c2[k] = (int16_t)P.csc2csr[k];
+        if (L.own_a) L.a[k] = aval(P, k, s);
+        if (L.own_pat) {
+            L.ri[k] = (int16_t)P.rowidx[k];
+            L.c2[k] = (int16_t)P.csc2csr[k];
+        }
         L.ci[k] = (int16_t)P.colidx[k];
     }
     for (int j = WG_TID; j <= n; j += WG_NT) L.cp[j] = (int16_t)P.colptr[j];

@@ -58,5 +58,10 @@ case "$1" in
           "bench:r05_s15_c2:--only C2 $A" "bench:r05_s15_c2_wf0:--only C2 $A --so {\"wg_first\":0}" ;;
   s16) # the whole GPU suite, then the driver's default command
        $J "test:tests" && $J "bench:r05_s16_default:--detail gpurun_out/r05_s16_default_detail.json" ;;
+  s17) # the workgroup solver's split layout with the shared pattern / A (PHX_WG_SPLIT=1): parity, C5a / C2 against the all-LDS layout, HBM bytes
+       PHX_WG_SPLIT=1 $J "test:tests/test_sslp.py tests/test_bench_settings.py tests/test_trajectories.py tests/test_gpu_parity.py" \
+          "bench:r05_s17_c5a_split:--only C5a $A" "bench:r05_s17_c2_split:--only C2 $A" \
+          "pmc:r05_pmc_c5a_split_fetch:FETCH_SIZE:--only C5a $A" "pmc:r05_pmc_c5a_split_write:WRITE_SIZE:--only C5a $A" && \
+       $J "bench:r05_s17_c5a:--only C5a $A" "bench:r05_s17_c2:--only C2 $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
