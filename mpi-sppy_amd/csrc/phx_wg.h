@@ -611,9 +611,14 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
         L.cc[j] = c;
         L.xp[j] = c == 1 ? l : (c == 2 ? u : x);
     }
-    for (int i = WG_TID; i < m; i += WG_NT) {
+    // (rows: a quad each, the row's entries interleaved over its four threads --
+    // farmer cm=10's land row has 30, sslp's facility rows 47: one thread per row
+    // made them the phase's serial chain)
+    for (int i = WG_QID; i < m; i += WG_QN) {
         double ax = 0.0;
-        for (int k = rp[i]; k < rp[i + 1]; ++k) ax += L.a[k] * St.xT[ix(ci[k], s, S)];
+        for (int k = rp[i] + WG_QL; k < rp[i + 1]; k += WG_QW) ax += L.a[k] * St.xT[ix(ci[k], s, S)];
+        ax = wg_quad_sum(ax);
+        if (WG_QL != 0) continue;
         const double bl = P.bl.at(i, s), bu = P.bu.at(i, s);
         const double yv = St.yT[ix(i, s, S)];
         int8_t r = 0;
@@ -665,14 +670,18 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
                 const int i = e / ld, k = e - i * ld;
                 L.Sm[e] = (i == k) ? reg : 0.0;
             }
+            // (P_FF + reg)^-1 per column, 0 on the non-free ones: one division per
+            // column instead of one per shared-column triple (L.r1 is free here:
+            // the refinement's first step rewrites it)
+            for (int j = WG_TID; j < n; j += WG_NT) L.r1[j] = L.cc[j] == 0 ? 1.0 / (L.pp[j] + reg) : 0.0;
             WG_SYNC();
             for (int p = WG_TID; p < G.npair; p += WG_NT) {
                 const int pa = L.pos[G.ia[p]], pb = L.pos[G.ib[p]];
                 if (pa < 0 || pb < 0) continue;
                 double v = 0.0;
                 for (int t = G.ptr[p]; t < G.ptr[p + 1]; ++t) {
-                    const int ka = G.ka[t], j = ci[ka];
-                    if (L.cc[j] == 0) v += L.a[ka] * L.a[G.kb[t]] / (L.pp[j] + reg);
+                    const int ka = G.ka[t];
+                    v += L.a[ka] * L.a[G.kb[t]] * L.r1[ci[ka]];
                 }
                 L.Sm[pa * ld + pb] += v;
             }
@@ -785,23 +794,31 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
         // ---- iterative refinement on the unregularised KKT (a proximal-point
         //      iteration) ----
         for (int it = 0; it < O.refine_steps; ++it) {
+            // r1 = H^-1 (-q - P x - A'z) on the free columns, 0 elsewhere (the
+            // division by the column's owner, once; the rows' products below
+            // then need none)
             for (int j = WG_TID; j < n; j += WG_NT) {
                 if (L.cc[j]) { L.r1[j] = 0.0; continue; }
                 double atz = 0.0;
                 for (int k = cp[j]; k < cp[j + 1]; ++k) atz += L.a[c2[k]] * L.z[ri[k]];
-                L.r1[j] = -L.qq[j] - L.pp[j] * L.xp[j] - atz;
+                L.r1[j] = (-L.qq[j] - L.pp[j] * L.xp[j] - atz) / (L.pp[j] + reg);
             }
             WG_SYNC();
-            for (int q = WG_TID; q < ma; q += WG_NT) {
+            // t = A_R (x + H^-1 r) - b_R: a quad per active row
+            for (int q = WG_QID; q < ma; q += WG_QN) {
                 const int i = L.ar[q];
                 double adr = 0.0, ax = 0.0;
-                for (int k = rp[i]; k < rp[i + 1]; ++k) {
+                for (int k = rp[i] + WG_QL; k < rp[i + 1]; k += WG_QW) {
                     const int j = ci[k];
                     ax += L.a[k] * L.xp[j];
-                    if (!L.cc[j]) adr += L.a[k] * L.r1[j] / (L.pp[j] + reg);
+                    adr += L.a[k] * L.r1[j];
                 }
-                const double b = L.rc[i] == 1 ? P.bl.at(i, s) : P.bu.at(i, s);
-                L.t[q] = adr - (b - ax);
+                ax = wg_quad_sum(ax);
+                adr = wg_quad_sum(adr);
+                if (WG_QL == 0) {
+                    const double b = L.rc[i] == 1 ? P.bl.at(i, s) : P.bu.at(i, s);
+                    L.t[q] = adr - (b - ax);
+                }
             }
             WG_SYNC();
             if (BLK == 2) {
@@ -856,7 +873,7 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
                     const int q = L.pos[ri[k]];
                     if (q >= 0) atz += L.a[c2[k]] * dz[q];
                 }
-                const double dx = (L.r1[j] - atz) / (L.pp[j] + reg);
+                const double dx = L.r1[j] - atz / (L.pp[j] + reg);
                 const double x = L.xp[j] + dx;
                 L.xp[j] = x;
                 dmax = fmax(dmax, fabs(dx));
@@ -899,9 +916,11 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
                 if (c == 2 && lam > dtol) bad = true;
             }
         }
-        for (int i = WG_TID; i < m; i += WG_NT) {
+        for (int i = WG_QID; i < m; i += WG_QN) {
             double ax = 0.0;
-            for (int k = rp[i]; k < rp[i + 1]; ++k) ax += L.a[k] * L.xp[ci[k]];
+            for (int k = rp[i] + WG_QL; k < rp[i + 1]; k += WG_QW) ax += L.a[k] * L.xp[ci[k]];
+            ax = wg_quad_sum(ax);
+            if (WG_QL != 0) continue;
             L.u[i] = ax;
             const double dr = P.dr[i];
             const double bl = P.bl.at(i, s), bu = P.bu.at(i, s);
