@@ -56,6 +56,30 @@ namespace phx {
 #define SP_SYNC() ((void)0)
 #endif
 
+// Separator rows are the long ones (netdes: the 50 flow balances, ~60 entries
+// each, against 2 in a capacity row; sslp: the 15 facility rows, 47 against 15):
+// with a thread per row they were each row phase's serial chain.  They get a
+// quad each instead (four adjacent threads, the row's entries interleaved,
+// combined by two lane shuffles), the B rows a thread each (sp_rows).
+#if defined(__HIP_DEVICE_COMPILE__)
+#define SP_QW 4
+#define SP_QL ((int)threadIdx.x & 3)
+#define SP_QID ((int)threadIdx.x >> 2)
+#define SP_QN ((int)blockDim.x >> 2)
+#else
+#define SP_QW 1
+#define SP_QL 0
+#define SP_QID 0
+#define SP_QN 1
+#endif
+PHX_HD double sp_quad_sum(double v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    v += __shfl_xor(v, 1, 64);
+    v += __shfl_xor(v, 2, 64);
+#endif
+    return v;
+}
+
 constexpr int SP_MAX_C = 64;      // separator rows: one wavefront's lanes (sp_csolve)
 constexpr int SP_RED = 16;        // reduction slots per value (<= 16 waves per workgroup)
 
@@ -157,6 +181,37 @@ PHX_HD double sp_a(const Prob& P, const SpSym& Y, int k, int s) {
     return v < 0 ? P.Ac[k] : Y.AvT[(int64_t)s * Y.nvar + v];
 }
 
+// A row phase: body(i, (A v1)_i, (A v2)_i) for every row i, the B rows by a
+// thread each, the separator rows by a quad each (every thread of the quad
+// computes the sums; body runs on the quad's first).  v2 null: 0.
+template <class F>
+PHX_HD void sp_rows(const Prob& P, const SpSym& Y, int s, const double* v1, const double* v2, F&& body) {
+    for (int i = SP_TID; i < P.m; i += SP_NT) {
+        if (Y.cpos[i] >= 0) continue;
+        double a1 = 0.0, a2 = 0.0;
+        for (int k = P.rowptr[i]; k < P.rowptr[i + 1]; ++k) {
+            const double a = sp_a(P, Y, k, s);
+            const int j = P.colidx[k];
+            a1 += a * v1[j];
+            if (v2) a2 += a * v2[j];
+        }
+        body(i, a1, a2);
+    }
+    for (int c = SP_QID; c < Y.nC; c += SP_QN) {
+        const int i = Y.crow[c];
+        double a1 = 0.0, a2 = 0.0;
+        for (int k = P.rowptr[i] + SP_QL; k < P.rowptr[i + 1]; k += SP_QW) {
+            const double a = sp_a(P, Y, k, s);
+            const int j = P.colidx[k];
+            a1 += a * v1[j];
+            if (v2) a2 += a * v2[j];
+        }
+        a1 = sp_quad_sum(a1);
+        if (v2) a2 = sp_quad_sum(a2);
+        if (SP_QL == 0) body(i, a1, a2);
+    }
+}
+
 // ---- workgroup reductions of K values (op 0 sum, 1 max, 2 min); the result in
 //      every thread, identical (commutative butterflies, fixed wave order) ----
 PHX_HD double sp_op(double a, double b, int op) { return op == 0 ? a + b : (op == 1 ? fmax(a, b) : fmin(a, b)); }
@@ -228,28 +283,49 @@ PHX_HD bool sp_factor_once(const Prob& P, const SpSym& Y, const SpScr& G, const 
         }
     }
     SP_SYNC();
-    // separator Schur complement (lower part, Sm[c1*ld + c2], c1 >= c2)
+    // separator Schur complement (lower part, Sm[c1*ld + c2], c1 >= c2): the
+    // off-diagonal entries a thread each (a few terms: the columns and B rows
+    // two separator rows share), the diagonal ones a quad each (every column
+    // and B row of the row: netdes ~60 + ~30 terms)
     for (int p = SP_TID; p < nC * nC; p += SP_NT) {
         const int c1 = p / nC, c2 = p - c1 * nC;
-        if (c2 > c1) continue;
+        if (c2 >= c1) continue;
         const double d1 = G.rdg[Y.crow[c1]], d2 = G.rdg[Y.crow[c2]];
-        double v;
-        if (d1 < 0.0 || d2 < 0.0) {
-            v = (c1 == c2) ? 1.0 : 0.0;
-            if (c1 == c2) L.cv[c1] = 1.0;
-        } else {
-            v = (c1 == c2) ? d1 : 0.0;
+        double v = 0.0;
+        if (!(d1 < 0.0 || d2 < 0.0)) {
             for (int t = Y.eap[p]; t < Y.eap[p + 1]; ++t) {
                 const int ka = Y.eka[t];
                 v += sp_a(P, Y, ka, s) * sp_a(P, Y, Y.ekb[t], s) * L.hv[P.colidx[ka]];
             }
-            if (c1 == c2) L.cv[c1] = v;      // M_cc: the reference of the pivot safeguard
             for (int t = Y.ebp[p]; t < Y.ebp[p + 1]; ++t) {
                 const int l1 = Y.el1[t];
                 v -= L.lv[l1] * L.lv[Y.el2[t]] / L.Mbb[Y.lrow[l1]];
             }
         }
         L.Sm[c1 * ld + c2] = v;
+    }
+    for (int c = SP_QID; c < nC; c += SP_QN) {
+        const int p = c * nC + c;
+        const double d1 = G.rdg[Y.crow[c]];
+        if (d1 < 0.0) {
+            if (SP_QL == 0) { L.Sm[c * ld + c] = 1.0; L.cv[c] = 1.0; }
+            continue;
+        }
+        double v = 0.0, w = 0.0;
+        for (int t = Y.eap[p] + SP_QL; t < Y.eap[p + 1]; t += SP_QW) {
+            const int ka = Y.eka[t];
+            v += sp_a(P, Y, ka, s) * sp_a(P, Y, Y.ekb[t], s) * L.hv[P.colidx[ka]];
+        }
+        for (int t = Y.ebp[p] + SP_QL; t < Y.ebp[p + 1]; t += SP_QW) {
+            const int l1 = Y.el1[t];
+            w += L.lv[l1] * L.lv[Y.el2[t]] / L.Mbb[Y.lrow[l1]];
+        }
+        v = d1 + sp_quad_sum(v);
+        w = sp_quad_sum(w);
+        if (SP_QL == 0) {
+            L.cv[c] = v;      // M_cc: the reference of the pivot safeguard
+            L.Sm[c * ld + c] = v - w;
+        }
     }
     SP_SYNC();
     // right-looking Cholesky, every trailing entry its own work item; L[i][k]
@@ -321,6 +397,14 @@ PHX_HD bool sp_factor_once(const Prob& P, const SpSym& Y, const SpScr& G, const 
     return true;
 }
 
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ double sp_readlane64(double v, int lane) {
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u & 0xffffffffull), lane);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), lane);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+#endif
 // S_C^-1 cv in place (forward + backward substitution), one wavefront: lane i
 // holds separator row i; the other waves wait at the closing barrier.
 PHX_HD void sp_csolve(const SpSym& Y, const SpLds& L) {
@@ -329,13 +413,15 @@ PHX_HD void sp_csolve(const SpSym& Y, const SpLds& L) {
     if (threadIdx.x < 64) {
         const int i = (int)threadIdx.x;
         double r = i < nC ? L.cv[i] : 0.0;
+        // (lane k's value by v_readlane -- k is uniform -- instead of a
+        // ds_bpermute shuffle: the substitution is a chain of 2 nC of them)
         for (int k = 0; k < nC; ++k) {
-            const double uk = __shfl(r, k, 64) * L.dg[k];
+            const double uk = sp_readlane64(r, k) * L.dg[k];
             if (i > k && i < nC) r -= L.Sm[k * ld + i] * uk;
             if (i == k) r = uk;
         }
         for (int k = nC - 1; k >= 0; --k) {
-            const double tk = __shfl(r, k, 64) * L.dg[k];
+            const double tk = sp_readlane64(r, k) * L.dg[k];
             if (i < k) r -= L.Sm[i * ld + k] * tk;
             if (i == k) r = tk;
         }
@@ -359,14 +445,16 @@ PHX_HD void sp_csolve(const SpSym& Y, const SpLds& L) {
 // M t = r with r in L.tv (rows), solution in L.tv.  Inactive rows: t = r.
 PHX_HD void sp_msolve(const Prob& P, const SpSym& Y, const SpLds& L) {
     const int nC = Y.nC;
-    for (int c = SP_TID; c < nC; c += SP_NT) {
-        double v = L.tv[Y.crow[c]];
-        for (int q = Y.clp[c]; q < Y.clp[c + 1]; ++q) {
+    // (a quad per separator row: its links -- netdes ~30 B rows -- interleaved)
+    for (int c = SP_QID; c < nC; c += SP_QN) {
+        double v = 0.0;
+        for (int q = Y.clp[c] + SP_QL; q < Y.clp[c + 1]; q += SP_QW) {
             const int l = Y.cll[q];
             const int b = Y.lrow[l];
-            v -= L.lv[l] * L.tv[b] / L.Mbb[b];
+            v += L.lv[l] * L.tv[b] / L.Mbb[b];
         }
-        L.cv[c] = v;
+        v = sp_quad_sum(v);
+        if (SP_QL == 0) L.cv[c] = L.tv[Y.crow[c]] - v;
     }
     SP_SYNC();
     sp_csolve(Y, L);
@@ -409,9 +497,7 @@ PHX_HD double sp_load(const Prob& P, const SpScr& G, const SpLds& L, int s) {
 // leaves A x in G.ax and A'y in G.aty.
 PHX_HD double sp_kkt_error(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds& L, int s) {
     double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};   // rp2 bn2 rd2 qn2 pobj dobj
-    for (int i = SP_TID; i < P.m; i += SP_NT) {
-        double ax = 0.0;
-        for (int k = P.rowptr[i]; k < P.rowptr[i + 1]; ++k) ax += sp_a(P, Y, k, s) * L.xv[P.colidx[k]];
+    sp_rows(P, Y, s, L.xv, nullptr, [&](int i, double ax, double) {
         G.ax[i] = ax;
         const double dr = P.dr[i], bl = G.bl[i], bu = G.bu[i];
         const double axu = ax / dr;
@@ -422,7 +508,7 @@ PHX_HD double sp_kkt_error(const Prob& P, const SpSym& Y, const SpScr& G, const 
         const double y = L.yv[i];
         if (y > 0.0 && isfinite(bl)) acc[5] += bl * y;
         else if (y < 0.0 && isfinite(bu)) acc[5] += bu * y;
-    }
+    });
     for (int j = SP_TID; j < P.n; j += SP_NT) {
         double aty = 0.0;
         for (int k = P.colptr[j]; k < P.colptr[j + 1]; ++k)
@@ -467,11 +553,9 @@ PHX_HD void sp_direction(const Prob& P, const SpSym& Y, const SpScr& G, const Sp
         L.hv[j] = (rho - rd) / G.hx[j];
     }
     SP_SYNC();
-    for (int i = SP_TID; i < P.m; i += SP_NT) {
+    sp_rows(P, Y, s, L.hv, nullptr, [&](int i, double adr, double) {
         const double bl = G.bl[i], bu = G.bu[i];
         const double ax = G.ax[i];
-        double adr = 0.0;
-        for (int k = P.rowptr[i]; k < P.rowptr[i + 1]; ++k) adr += sp_a(P, Y, k, s) * L.hv[P.colidx[k]];
         double rhs;
         if (!isfinite(bl) && !isfinite(bu)) {
             rhs = 0.0;
@@ -489,7 +573,7 @@ PHX_HD void sp_direction(const Prob& P, const SpSym& Y, const SpScr& G, const Sp
             rhs = -(ax - sv) + rhos / sig - adr;
         }
         L.tv[i] = rhs;
-    }
+    });
     SP_SYNC();
     sp_msolve(P, Y, L);
     for (int i = SP_TID; i < P.m; i += SP_NT) {
@@ -564,10 +648,8 @@ PHX_HD double sp_ipm(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds&
         G.dzl[j] = G.dzu[j] = 0.0;
     }
     SP_SYNC();
-    for (int i = SP_TID; i < m; i += SP_NT) {
+    sp_rows(P, Y, s, L.xv, nullptr, [&](int i, double ax, double) {
         const double bl = G.bl[i], bu = G.bu[i];
-        double ax = 0.0;
-        for (int k = P.rowptr[i]; k < P.rowptr[i + 1]; ++k) ax += sp_a(P, Y, k, s) * L.xv[P.colidx[k]];
         double sv;
         const bool eq = (bl == bu);
         if (eq) sv = bl;
@@ -578,7 +660,7 @@ PHX_HD double sp_ipm(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds&
         G.wu[i] = (isfinite(bu) && !eq) ? 1.0 : 0.0;
         G.dwl[i] = G.dwu[i] = 0.0;
         L.yv[i] = G.wl[i] - G.wu[i];
-    }
+    });
     SP_SYNC();
     double err = 1e300;
     int it = 0;
@@ -719,16 +801,14 @@ PHX_HD void sp_classify(const Prob& P, const SpSym& Y, const SpScr& G, const SpL
         G.cc[j] = c;
         G.dx[j] = c == 1 ? l : (c == 2 ? u : x);
     }
-    for (int i = SP_TID; i < P.m; i += SP_NT) {
-        double ax = 0.0;
-        for (int k = P.rowptr[i]; k < P.rowptr[i + 1]; ++k) ax += sp_a(P, Y, k, s) * L.xv[P.colidx[k]];
+    sp_rows(P, Y, s, L.xv, nullptr, [&](int i, double ax, double) {
         const double bl = G.bl[i], bu = G.bu[i], yv = L.yv[i];
         int r = 0;
         if (isfinite(bl) && (ax - bl <= tol * (1.0 + fabs(bl)) || ax - bl < yv)) r = 1;
         else if (isfinite(bu) && (bu - ax <= tol * (1.0 + fabs(bu)) || bu - ax < -yv)) r = 2;
         G.rc[i] = r;
         G.ds[i] = r ? -yv : 0.0;
-    }
+    });
     SP_SYNC();
     for (int j = SP_TID; j < P.n; j += SP_NT) L.xv[j] = G.dx[j];
     for (int i = SP_TID; i < P.m; i += SP_NT) L.yv[i] = G.ds[i];
@@ -761,19 +841,12 @@ PHX_HD int sp_rounds(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds&
                 L.hv[j] = r1 / (G.pp[j] + reg);
             }
             SP_SYNC();
-            for (int i = SP_TID; i < m; i += SP_NT) {
+            sp_rows(P, Y, s, L.xv, L.hv, [&](int i, double ax, double adr) {
                 const int rc = G.rc[i];
-                if (!rc) { L.tv[i] = 0.0; continue; }
-                double adr = 0.0, ax = 0.0;
-                for (int k = P.rowptr[i]; k < P.rowptr[i + 1]; ++k) {
-                    const double a = sp_a(P, Y, k, s);
-                    const int j = P.colidx[k];
-                    ax += a * L.xv[j];
-                    adr += a * L.hv[j];
-                }
+                if (!rc) { L.tv[i] = 0.0; return; }
                 const double b = rc == 1 ? G.bl[i] : G.bu[i];
                 L.tv[i] = adr - (b - ax);
-            }
+            });
             SP_SYNC();
             sp_msolve(P, Y, L);
             double mx[2] = {0.0, 0.0};   // max |correction|, max |value|
@@ -821,9 +894,7 @@ PHX_HD int sp_rounds(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds&
                 if (c == 2 && lam > dtol) bad[0] = 1.0;
             }
         }
-        for (int i = SP_TID; i < m; i += SP_NT) {
-            double ax = 0.0;
-            for (int k = P.rowptr[i]; k < P.rowptr[i + 1]; ++k) ax += sp_a(P, Y, k, s) * L.xv[P.colidx[k]];
+        sp_rows(P, Y, s, L.xv, nullptr, [&](int i, double ax, double) {
             G.ax[i] = ax;
             const double dr = P.dr[i], bl = G.bl[i], bu = G.bu[i];
             if (!(ax - ax == 0.0) || !(L.yv[i] - L.yv[i] == 0.0)) bad[0] = 1.0;
@@ -834,7 +905,7 @@ PHX_HD int sp_rounds(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds&
                 if (G.rc[i] == 1 && y < -dtol) bad[0] = 1.0;
                 if (G.rc[i] == 2 && y > dtol) bad[0] = 1.0;
             }
-        }
+        });
         sp_reduce<1>(bad, L.red, 1);
         if (bad[0] == 0.0) return round + 1;
         if (round + 1 == rounds) break;

@@ -63,9 +63,10 @@ case "$1" in
           "bench:r05_s17_c5a_split:--only C5a $A" "bench:r05_s17_c2_split:--only C2 $A" \
           "pmc:r05_pmc_c5a_split_fetch:FETCH_SIZE:--only C5a $A" "pmc:r05_pmc_c5a_split_write:WRITE_SIZE:--only C5a $A" && \
        $J "bench:r05_s17_c5a:--only C5a $A" "bench:r05_s17_c2:--only C2 $A" ;;
-  s18) # quad-per-row phases + hoisted (P+reg)^-1 in the workgroup solver, the split layout by default on C5a: parity, C5a / C2 (+ all-LDS C5a)
-       $J "test:tests/test_sslp.py tests/test_bench_settings.py tests/test_trajectories.py tests/test_gpu_parity.py" \
-          "bench:r05_s18_c5a:--only C5a $A" "bench:r05_s18_c2:--only C2 $A" && \
+  s18) # workgroup solver: a quad per row + (P+reg)^-1 per column, the split layout by default on C5a; sparse solver:
+       # separator rows / Schur diagonal / msolve links a quad each, readlane substitution -- parity, C5a / C2 / C5b (+ all-LDS C5a)
+       $J "test:tests/test_sslp.py tests/test_netdes.py tests/test_bench_settings.py tests/test_trajectories.py tests/test_gpu_parity.py" \
+          "bench:r05_s18_c5a:--only C5a $A" "bench:r05_s18_c2:--only C2 $A" "bench:r05_s18_c5b:--only C5b $A" && \
        PHX_WG_SPLIT=0 $J "bench:r05_s18_c5a_lds:--only C5a $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
