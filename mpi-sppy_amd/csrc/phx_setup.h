@@ -116,7 +116,9 @@ inline void build_seg_tiles(const std::vector<int32_t>& s0, const std::vector<in
 // shared column in both rows, in (ia, ib) order.  Built from the CSC view.
 struct WgPairsHost {
     std::vector<int32_t> ptr, ia, ib, ka, kb;
+    int32_t nlong = 0;    // the first nlong pairs share >= WG_LONG_PAIR columns
 };
+constexpr int WG_LONG_PAIR = 8;
 
 inline void build_wg_pairs(const HostSetup& hs, int n, int m, WgPairsHost& out) {
     std::vector<std::vector<std::pair<int32_t, int32_t>>> trip((size_t)m * m);
@@ -129,15 +131,21 @@ inline void build_wg_pairs(const HostSetup& hs, int n, int m, WgPairsHost& out) 
             }
     out = WgPairsHost{};
     out.ptr.push_back(0);
-    for (int ia = 0; ia < m; ++ia)
-        for (int ib = 0; ib <= ia; ++ib) {
-            const auto& t = trip[(size_t)ia * m + ib];
-            if (t.empty()) continue;
-            out.ia.push_back(ia);
-            out.ib.push_back(ib);
-            for (const auto& pr : t) { out.ka.push_back(pr.first); out.kb.push_back(pr.second); }
-            out.ptr.push_back((int32_t)out.ka.size());
-        }
+    // the long pairs first (a row with itself: every column of the row --
+    // farmer cm=10's land row 30, sslp's facility rows 47), the rest after
+    // (wg_warm gives the long ones a quad each, the others a thread)
+    for (int pass = 0; pass < 2; ++pass) {
+        for (int ia = 0; ia < m; ++ia)
+            for (int ib = 0; ib <= ia; ++ib) {
+                const auto& t = trip[(size_t)ia * m + ib];
+                if (t.empty() || ((int)t.size() >= WG_LONG_PAIR) != (pass == 0)) continue;
+                out.ia.push_back(ia);
+                out.ib.push_back(ib);
+                for (const auto& pr : t) { out.ka.push_back(pr.first); out.kb.push_back(pr.second); }
+                out.ptr.push_back((int32_t)out.ka.size());
+            }
+        if (pass == 0) out.nlong = (int32_t)out.ia.size();
+    }
 }
 
 // Symbolic structure of the sparse workgroup solver (phx_sp.h SpSym): rows

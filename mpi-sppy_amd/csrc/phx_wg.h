@@ -57,7 +57,7 @@ namespace phx {
 // positions (ka in row ia, kb in row ib) of every shared column, built once on
 // the host from the pattern (phx_set_problem).
 struct WgPairs {
-    int32_t npair;
+    int32_t npair;        // (the first nlong share many columns: a quad each in wg_warm)
     const int32_t* ptr;   // [npair+1] into ka/kb
     const int32_t* ia;    // [npair]
     const int32_t* ib;    // [npair]
@@ -85,6 +85,7 @@ struct WgPairs {
     const int16_t* pat_c2 = nullptr;
     const double* a_const = nullptr;
     int32_t single_after = WG_SINGLE_AFTER;   // rounds of full primal-dual changes before single ones
+    int32_t nlong = 0;    // pairs [0, nlong) are the long ones (phx_setup.h build_wg_pairs)
 };
 
 // Carve of the dynamic LDS of one scenario.
@@ -675,7 +676,20 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
             // the refinement's first step rewrites it)
             for (int j = WG_TID; j < n; j += WG_NT) L.r1[j] = L.cc[j] == 0 ? 1.0 / (L.pp[j] + reg) : 0.0;
             WG_SYNC();
-            for (int p = WG_TID; p < G.npair; p += WG_NT) {
+            // (the long pairs -- a row with itself -- a quad each, their shared
+            // columns interleaved; the others a thread each)
+            for (int p = WG_QID; p < G.nlong; p += WG_QN) {
+                const int pa = L.pos[G.ia[p]], pb = L.pos[G.ib[p]];
+                if (pa < 0 || pb < 0) continue;
+                double v = 0.0;
+                for (int t = G.ptr[p] + WG_QL; t < G.ptr[p + 1]; t += WG_QW) {
+                    const int ka = G.ka[t];
+                    v += L.a[ka] * L.a[G.kb[t]] * L.r1[ci[ka]];
+                }
+                v = wg_quad_sum(v);
+                if (WG_QL == 0) L.Sm[pa * ld + pb] += v;
+            }
+            for (int p = G.nlong + WG_TID; p < G.npair; p += WG_NT) {
                 const int pa = L.pos[G.ia[p]], pb = L.pos[G.ib[p]];
                 if (pa < 0 || pb < 0) continue;
                 double v = 0.0;

@@ -68,5 +68,9 @@ case "$1" in
        $J "test:tests/test_sslp.py tests/test_netdes.py tests/test_bench_settings.py tests/test_trajectories.py tests/test_gpu_parity.py" \
           "bench:r05_s18_c5a:--only C5a $A" "bench:r05_s18_c2:--only C2 $A" "bench:r05_s18_c5b:--only C5b $A" && \
        PHX_WG_SPLIT=0 $J "bench:r05_s18_c5a_lds:--only C5a $A" ;;
+  s19) # workgroup solver: the long Schur pairs a quad each; phase clocks (PHX_WG_PROF) of C2 / C5a
+       $J "test:tests/test_sslp.py tests/test_bench_settings.py tests/test_gpu_parity.py" \
+          "bench:r05_s19_c2:--only C2 $A" "bench:r05_s19_c5a:--only C5a $A" && \
+       PHX_WG_PROF=1 $J "bench:r05_s19_c2_wgprof:--only C2 $A" "bench:r05_s19_c5a_wgprof:--only C5a $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
