@@ -818,6 +818,7 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
                 L.r1[j] = (-L.qq[j] - L.pp[j] * L.xp[j] - atz) / (L.pp[j] + reg);
             }
             WG_SYNC();
+            WG_TP(11);
             // t = A_R (x + H^-1 r) - b_R: a quad per active row
             for (int q = WG_QID; q < ma; q += WG_QN) {
                 const int i = L.ar[q];
@@ -835,6 +836,7 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
                 }
             }
             WG_SYNC();
+            WG_TP(12);
             if (BLK == 2) {
                 // dz = M^-1 t (full rows; compact order) into u
                 for (int i = WG_QID; i < ma; i += WG_QN) {
@@ -878,6 +880,7 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
             }
             WG_SYNC();
             }
+            WG_TP(13);
             const double* dz = BLK == 2 ? L.u : L.t;
             double dmax = 0.0, xmax = 0.0;
             for (int j = WG_TID; j < n; j += WG_NT) {
@@ -903,6 +906,7 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
             // stop once the correction vanishes (phx_lane.h kkt_refine's rule)
             wg_max2(dmax, xmax, L.red);
             const bool done = dmax <= 1e-10 * (1.0 + xmax);
+            WG_TP(14);
             WG_CNT(8);
             if (done) break;
         }

@@ -72,5 +72,9 @@ case "$1" in
        $J "test:tests/test_sslp.py tests/test_bench_settings.py tests/test_gpu_parity.py" \
           "bench:r05_s19_c2:--only C2 $A" "bench:r05_s19_c5a:--only C5a $A" && \
        PHX_WG_PROF=1 $J "bench:r05_s19_c2_wgprof:--only C2 $A" "bench:r05_s19_c5a_wgprof:--only C5a $A" ;;
+  s20) # workgroup solver: refinement sub-phase clocks (C2, C5a); C2 with the blocked MFMA factor (PHX_WG_BLK=1) against the scalar one
+       PHX_WG_PROF=1 $J "bench:r05_s20_c2_wgprof:--only C2 $A" "bench:r05_s20_c5a_wgprof:--only C5a $A" && \
+       PHX_WG_BLK=1 $J "bench:r05_s20_c2_blk1:--only C2 $A" && PHX_WG_BLK=1 PHX_WG_PROF=1 $J "bench:r05_s20_c2_blk1_wgprof:--only C2 $A" && \
+       $J "bench:r05_s20_c2:--only C2 $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
