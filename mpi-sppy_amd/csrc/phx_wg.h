@@ -86,6 +86,7 @@ struct WgPairs {
     const double* a_const = nullptr;
     int32_t single_after = WG_SINGLE_AFTER;   // rounds of full primal-dual changes before single ones
     int32_t nlong = 0;    // pairs [0, nlong) are the long ones (phx_setup.h build_wg_pairs)
+    int32_t prof_off = 0; // byte offset of the profiler's 16 LDS slots (after the carve; PHX_WG_PROF)
 };
 
 // Carve of the dynamic LDS of one scenario.
@@ -238,18 +239,21 @@ PHX_HD double wg_quad_sum(double v) {
 }
 
 // Optional phase timing (PHX_WG_PROF=1 on the host side): per phase, the
-// shader-clock cycles summed over the lanes' wavefronts (thread 0 of each).
+// shader-clock cycles of the workgroup's thread 0, accumulated in 16 LDS slots
+// (prof: k_wg_warm's, after the carve) and added to the global sums once at the
+// kernel's end -- a global atomic per phase stalled the next barrier behind
+// 1,000 workgroups' atomics on the same 16 words and moved time between phases.
 #if defined(__HIP_DEVICE_COMPILE__)
 #define WG_T0() long long _wg_t = prof ? clock64() : 0
 #define WG_TP(ph)                                                             \
     do {                                                                      \
         if (prof && threadIdx.x == 0) {                                       \
             const long long _n = clock64();                                   \
-            atomicAdd(prof + (ph), (unsigned long long)(_n - _wg_t));         \
+            prof[ph] += (unsigned long long)(_n - _wg_t);                     \
             _wg_t = _n;                                                       \
         }                                                                     \
     } while (0)
-#define WG_CNT(ph) do { if (prof && threadIdx.x == 0) atomicAdd(prof + (ph), 1ull); } while (0)
+#define WG_CNT(ph) do { if (prof && threadIdx.x == 0) prof[ph] += 1ull; } while (0)
 #else
 #define WG_T0() (void)prof
 #define WG_TP(ph) ((void)0)

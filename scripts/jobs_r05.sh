@@ -76,5 +76,8 @@ case "$1" in
        PHX_WG_PROF=1 $J "bench:r05_s20_c2_wgprof:--only C2 $A" "bench:r05_s20_c5a_wgprof:--only C5a $A" && \
        PHX_WG_BLK=1 $J "bench:r05_s20_c2_blk1:--only C2 $A" && PHX_WG_BLK=1 PHX_WG_PROF=1 $J "bench:r05_s20_c2_blk1_wgprof:--only C2 $A" && \
        $J "bench:r05_s20_c2:--only C2 $A" ;;
+  s21) # workgroup phase clocks accumulated in LDS (one global add per workgroup): C2 (scalar, blocked) / C5a, and C2 unprofiled
+       PHX_WG_PROF=1 $J "bench:r05_s21_c2_wgprof:--only C2 $A" "bench:r05_s21_c5a_wgprof:--only C5a $A" && \
+       PHX_WG_BLK=1 PHX_WG_PROF=1 $J "bench:r05_s21_c2_blk1_wgprof:--only C2 $A" && $J "bench:r05_s21_c2:--only C2 $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
