@@ -563,71 +563,6 @@ PHX_HD void wg_blk_lauum(double* Sm, int ld, int ma) {
 }
 #endif
 
-// dz = M^-1 t for M = L L^T (the factor as the scalar and blocked Cholesky leave
-// it: L[i][k], i > k, at Sm[k*ld + i], 1 / L_kk in dg), t in L.t (compact
-// order), the result in place: forward then backward substitution on wavefront
-// 0, lane i holding row i (ma <= 64), lane k's value broadcast by v_readlane
-// (k is uniform); the factor's entries are read eight steps at a time ahead of
-// the chain.  The other wavefronts wait at the closing barrier.
-#define WG_TRI_MAX 64
-PHX_HD void wg_trsolve(const WgLds& L, int ma, int ld) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    if (threadIdx.x < 64) {
-        const int i = (int)threadIdx.x;
-        const bool in = i < ma;
-        const double di = in ? L.dg[i] : 0.0;
-        double r = in ? L.t[i] : 0.0;
-        // r_i -= L[i][k] u_k, u_k = r_k / L_kk (lane k scales its own first)
-        for (int k0 = 0; k0 < ma; k0 += 8) {
-            double lk[8];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const int k = k0 + q;
-                const bool use = in && k < ma && i > k;
-                lk[q] = L.Sm[(use ? k : 0) * ld + (use ? i : 0)];
-                lk[q] = use ? lk[q] : 0.0;
-            }
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const int k = k0 + q;
-                if (k >= ma) break;
-                if (i == k) r *= di;
-                r = fma(-lk[q], wg_readlane64(r, k), r);    // (lk = 0 on lanes i <= k)
-            }
-        }
-        // r_i -= L[k][i] x_k for k > i, x_k = r_k / L_kk
-        for (int k0 = ma - 1; k0 >= 0; k0 -= 8) {
-            double lk[8];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const int k = k0 - q;
-                const bool use = in && k >= 0 && i < k;
-                lk[q] = L.Sm[(use ? i : 0) * ld + (use ? k : 0)];
-                lk[q] = use ? lk[q] : 0.0;
-            }
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const int k = k0 - q;
-                if (k < 0) break;
-                if (i == k) r *= di;
-                r = fma(-lk[q], wg_readlane64(r, k), r);
-            }
-        }
-        if (in) L.t[i] = r;
-    }
-    __syncthreads();
-#else
-    for (int k = 0; k < ma; ++k) {
-        L.t[k] *= L.dg[k];
-        for (int i = k + 1; i < ma; ++i) L.t[i] = fma(-L.Sm[k * ld + i], L.t[k], L.t[i]);
-    }
-    for (int k = ma - 1; k >= 0; --k) {
-        L.t[k] *= L.dg[k];
-        for (int i = 0; i < k; ++i) L.t[i] = fma(-L.Sm[i * ld + k], L.t[k], L.t[i]);
-    }
-#endif
-}
-
 // Returns (uniformly) the number of rounds the lane used when the point in
 // L.xp / L.z passes the KKT certificate, else 0; rounds > 1 allow primal-dual
 // active-set updates in between.
@@ -706,11 +641,6 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
         WG_SYNC();
         const int ma = L.flag[3];
         const int ld = ma | 1;
-        // tri: the refinement solves with the factor itself, by substitution on
-        // one wavefront (wg_trsolve), instead of forming L^-1 (BLK 0: the
-        // explicit inverse, BLK 1: wg_blk_trtri) -- round 5: the inverse was a
-        // quarter of farmer cm=10's workgroup pass, its ma-step column chains
-        const bool tri = BLK != 2 && ma <= WG_TRI_MAX;
         // ---- the cached factor of this active set and prox weights, if any ----
         const bool cache = G.fac != nullptr;
         bool reused = false;
@@ -725,15 +655,12 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
             if (diff) L.flag[1] = 1;
             WG_SYNC();
             if (L.flag[1] == 0) {
-                // (the refinement reads only L^-1, the lower triangle -- or with
-                // tri the factor: L^T in the upper part and 1 / L_kk after it)
+                // (the refinement reads only L^-1, the lower triangle)
                 const double* f = G.fac + (int64_t)s * G.fac_stride;
                 for (int e = WG_TID; e < ma * ld; e += WG_NT) {
                     const int i = e / ld, c = e - i * ld;
-                    if (tri ? (c > i && c < ma) : (BLK == 2 ? c < ma : c <= i)) L.Sm[e] = f[e];
+                    if (BLK == 2 ? c < ma : c <= i) L.Sm[e] = f[e];
                 }
-                if (tri)
-                    for (int k = WG_TID; k < ma; k += WG_NT) L.dg[k] = f[ma * ld + k];
                 WG_SYNC();
                 WG_CNT(10);
                 reused = true;
@@ -781,7 +708,7 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
           if (BLK) {
             if (!wg_blk_cholesky(L.Sm, ld, ma, L.dg, L.flag + 2)) return 0;
             WG_TP(2);
-            if (!tri) wg_blk_trtri(L.Sm, ld, ma, L.dg);
+            wg_blk_trtri(L.Sm, ld, ma, L.dg);
             if (BLK == 2) wg_blk_lauum(L.Sm, ld, ma);
             WG_TP(3);
           } else {
@@ -865,7 +792,7 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
             // combined inside the quad; every thread of the quad holds the new
             // entry and writes the same value, so the next step's reads of it
             // by the other three need no ordering beyond their own store)
-            for (int c = WG_QID; c < (tri ? 0 : ma); c += WG_QN) {
+            for (int c = WG_QID; c < ma; c += WG_QN) {
                 if (WG_QL == 0) L.Sm[c * ld + c] = L.dg[c];
                 for (int i = c + 1; i < ma; ++i) {
                     double v0 = WG_QL == 0 ? L.Sm[c * ld + i] * L.dg[c] : 0.0, v1 = 0.0;
@@ -929,9 +856,6 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
                     if (WG_QL == 0) L.u[i] = v;
                 }
                 WG_SYNC();
-            } else if (tri) {
-                // dz = L^-T L^-1 t in place, one wavefront
-                wg_trsolve(L, ma, ld);
             } else {
             // u = L^-1 t ; then t = L^-T u (dz, compact order)
             for (int i = WG_QID; i < ma; i += WG_QN) {
@@ -1051,10 +975,8 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
                 double* f = G.fac + (int64_t)s * G.fac_stride;
                 for (int e = WG_TID; e < ma * ld; e += WG_NT) {
                     const int i = e / ld, c = e - i * ld;
-                    if (tri ? (c > i && c < ma) : (BLK == 2 ? c < ma : c <= i)) f[e] = L.Sm[e];
+                    if (BLK == 2 ? c < ma : c <= i) f[e] = L.Sm[e];
                 }
-                if (tri)
-                    for (int k = WG_TID; k < ma; k += WG_NT) f[ma * ld + k] = L.dg[k];
                 int8_t* kc = G.key + (int64_t)s * G.key_stride;
                 double* pk = G.pkey + (int64_t)s * (G.N + 1);
                 for (int j = WG_TID; j < n; j += WG_NT) kc[j] = L.cc[j];

@@ -79,9 +79,5 @@ case "$1" in
   s21) # workgroup phase clocks accumulated in LDS (one global add per workgroup): C2 (scalar, blocked) / C5a, and C2 unprofiled
        PHX_WG_PROF=1 $J "bench:r05_s21_c2_wgprof:--only C2 $A" "bench:r05_s21_c5a_wgprof:--only C5a $A" && \
        PHX_WG_BLK=1 PHX_WG_PROF=1 $J "bench:r05_s21_c2_blk1_wgprof:--only C2 $A" && $J "bench:r05_s21_c2:--only C2 $A" ;;
-  s22) # workgroup solver: the refinement by substitution with the factor (wg_trsolve), no L^-1 -- parity, C2 / C5a, phase clocks
-       $J "test:tests/test_sslp.py tests/test_bench_settings.py tests/test_trajectories.py tests/test_gpu_parity.py tests/test_wg_blk.py" \
-          "bench:r05_s22_c2:--only C2 $A" "bench:r05_s22_c5a:--only C5a $A" && \
-       PHX_WG_PROF=1 $J "bench:r05_s22_c2_wgprof:--only C2 $A" "bench:r05_s22_c5a_wgprof:--only C5a $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
