@@ -786,13 +786,19 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
                 return 0;
             }
             WG_TP(2);
-            // ---- explicit inverse of L into the lower part (diagonal included):
-            //      one column per thread, no cross-thread dependence ----
-            // (a quad per column c: interleaved k, two partial sums per thread,
-            // combined inside the quad; every thread of the quad holds the new
-            // entry and writes the same value, so the next step's reads of it
-            // by the other three need no ordering beyond their own store)
-            for (int c = WG_QID; c < ma; c += WG_QN) {
+            // ---- explicit inverse of L into the lower part (diagonal included).
+            //      Round 5: the blocked MFMA inverse (wg_blk_trtri) after the
+            //      scalar factor when it fits its tiles -- farmer cm=10: the
+            //      scalar inverse's ma-step column chains took 731 against the
+            //      blocked one's 311 Mcycles per ten passes (r05 s21), while the
+            //      scalar factor beats the blocked one (796 against 1,423) ----
+            const bool blk_inv = ma <= WG_BLK_MAX;
+            if (blk_inv) wg_blk_trtri(L.Sm, ld, ma, L.dg);
+            // (the scalar inverse: a quad per column c, interleaved k, two partial
+            // sums per thread, combined inside the quad; every thread of the quad
+            // holds the new entry and writes the same value, so the next step's
+            // reads of it by the other three need no ordering beyond their own store)
+            for (int c = WG_QID; c < (blk_inv ? 0 : ma); c += WG_QN) {
                 if (WG_QL == 0) L.Sm[c * ld + c] = L.dg[c];
                 for (int i = c + 1; i < ma; ++i) {
                     double v0 = WG_QL == 0 ? L.Sm[c * ld + i] * L.dg[c] : 0.0, v1 = 0.0;

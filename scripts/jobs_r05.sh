@@ -79,5 +79,14 @@ case "$1" in
   s21) # workgroup phase clocks accumulated in LDS (one global add per workgroup): C2 (scalar, blocked) / C5a, and C2 unprofiled
        PHX_WG_PROF=1 $J "bench:r05_s21_c2_wgprof:--only C2 $A" "bench:r05_s21_c5a_wgprof:--only C5a $A" && \
        PHX_WG_BLK=1 PHX_WG_PROF=1 $J "bench:r05_s21_c2_blk1_wgprof:--only C2 $A" && $J "bench:r05_s21_c2:--only C2 $A" ;;
+  s22) # (measured and reverted) the refinement by one-wavefront substitution with the factor instead of L^-1: C2 / C5a + phase clocks
+       $J "test:tests/test_sslp.py tests/test_bench_settings.py tests/test_trajectories.py tests/test_gpu_parity.py tests/test_wg_blk.py" \
+          "bench:r05_s22_c2:--only C2 $A" "bench:r05_s22_c5a:--only C5a $A" && \
+       PHX_WG_PROF=1 $J "bench:r05_s22_c2_wgprof:--only C2 $A" "bench:r05_s22_c5a_wgprof:--only C5a $A" ;;
+  s23) # workgroup solver: scalar factor + blocked MFMA inverse (BLK 0) -- parity, C2; C5a blocked (default) against BLK 0; phase clocks
+       $J "test:tests/test_sslp.py tests/test_bench_settings.py tests/test_trajectories.py tests/test_gpu_parity.py tests/test_wg_blk.py" \
+          "bench:r05_s23_c2:--only C2 $A" "bench:r05_s23_c5a:--only C5a $A" && \
+       PHX_WG_BLK=0 $J "bench:r05_s23_c5a_blk0:--only C5a $A" && \
+       PHX_WG_PROF=1 $J "bench:r05_s23_c2_wgprof:--only C2 $A" && PHX_WG_BLK=0 PHX_WG_PROF=1 $J "bench:r05_s23_c5a_blk0_wgprof:--only C5a $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
