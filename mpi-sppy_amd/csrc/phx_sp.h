@@ -117,7 +117,31 @@ struct SpLds {
     double *yv;    // [m] y (interior point) or z = -y (active set)
     double *tv;    // [m] row right-hand side / solution
     double *red;   // [8 * SP_RED] reduction slots
+    // PHX_SP_PROF: 16 LDS slots of thread 0's phase clocks (15: the last stamp),
+    // null when off (k_sp_solve_t / k_sp_polish add them to the global sums)
+    unsigned long long* prof = nullptr;
 };
+
+// Phase clocks (PHX_SP_PROF=1): the cycles since the last stamp go to phase ph.
+// Phases: 0 load / classify, 1 B rows + separator Schur assembly, 2 separator
+// Cholesky, 3-6 a refinement step's column residual, row products, M solve,
+// update + stop test, 7 certificate, 8 active-set update, 9-11 interior point:
+// KKT error + mu, a direction's products before / after its M solve (+ steps);
+// counters 12 refinement steps, 13 interior-point iterations, 14 rounds.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define SP_TP(ph)                                                                       \
+    do {                                                                                \
+        if (L.prof && threadIdx.x == 0) {                                               \
+            const unsigned long long _n = (unsigned long long)clock64();                \
+            L.prof[ph] += _n - L.prof[15];                                              \
+            L.prof[15] = _n;                                                            \
+        }                                                                               \
+    } while (0)
+#define SP_CNT(ph) do { if (L.prof && threadIdx.x == 0) L.prof[ph] += 1ull; } while (0)
+#else
+#define SP_TP(ph) ((void)0)
+#define SP_CNT(ph) ((void)0)
+#endif
 
 // Split layout (split = true): the link / B-row / column vectors (lv, Mbb,
 // hv, xv: nlink + m + 2n doubles) live in the workgroup's global scratch slot
@@ -328,6 +352,7 @@ PHX_HD bool sp_factor_once(const Prob& P, const SpSym& Y, const SpScr& G, const 
         }
     }
     SP_SYNC();
+    SP_TP(1);
     // right-looking Cholesky, every trailing entry its own work item; L[i][k]
     // (i > k) is stored transposed at Sm[k*ld + i], 1/L_kk in dg.
     // Pivots in pairs (a, b = a+1), one barrier per pair: every trailing
@@ -394,6 +419,7 @@ PHX_HD bool sp_factor_once(const Prob& P, const SpSym& Y, const SpScr& G, const 
         if (SP_TID == 0) L.dg[jj] = 1.0 / sd;
         SP_SYNC();
     }
+    SP_TP(2);
     return true;
 }
 
@@ -466,6 +492,7 @@ PHX_HD void sp_msolve(const Prob& P, const SpSym& Y, const SpLds& L) {
         L.tv[i] = v / L.Mbb[i];
     }
     SP_SYNC();
+    SP_TP(5);
 }
 
 // ---------------------------------------------------------------------------
@@ -575,6 +602,7 @@ PHX_HD void sp_direction(const Prob& P, const SpSym& Y, const SpScr& G, const Sp
         L.tv[i] = rhs;
     });
     SP_SYNC();
+    SP_TP(10);
     sp_msolve(P, Y, L);
     for (int i = SP_TID; i < P.m; i += SP_NT) {
         const double bl = G.bl[i], bu = G.bu[i];
@@ -599,6 +627,7 @@ PHX_HD void sp_direction(const Prob& P, const SpSym& Y, const SpScr& G, const Sp
         if (isfinite(l)) G.dzl[j] = (G.cl[j] - G.zl[j] * dxv) / (x - l);
         if (isfinite(u)) G.dzu[j] = (G.cu[j] + G.zu[j] * dxv) / (u - x);
     }
+    SP_TP(11);
 }
 
 PHX_HD void sp_steps(const Prob& P, const SpScr& G, const SpLds& L, double& ap, double& ad) {
@@ -635,6 +664,7 @@ PHX_HD void sp_steps(const Prob& P, const SpScr& G, const SpLds& L, double& ap, 
 PHX_HD double sp_ipm(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds& L, int s, int max_it,
                      double tol, double reg, int* its) {
     const int n = P.n, m = P.m;
+    SP_TP(0);
     for (int j = SP_TID; j < n; j += SP_NT) {
         const double l = G.lb[j], u = G.ub[j];
         double x;
@@ -680,6 +710,8 @@ PHX_HD double sp_ipm(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds&
             if (isfinite(bu)) { mu_acc[0] += (bu - sv) * G.wu[i]; mu_acc[1] += 1.0; }
         }
         sp_reduce<2>(mu_acc, L.red, 0);
+        SP_TP(9);
+        SP_CNT(13);
         const double ncomp = mu_acc[1];
         const double mu = ncomp > 0.0 ? mu_acc[0] / ncomp : 0.0;
         if (err < tol || !(err < 1e300)) break;
@@ -777,6 +809,7 @@ PHX_HD double sp_ipm(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds&
             L.yv[i] += ad * L.tv[i];
         }
         SP_SYNC();
+        SP_TP(11);
     }
     *its = it;
     return err;
@@ -824,7 +857,9 @@ PHX_HD int sp_rounds(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds&
     const double reg = O.reg;
     const double dtol = O.kkt_tol * (1.0 + qmax);
     const double ptol = O.kkt_tol;
+    SP_TP(0);
     for (int round = 0; round < rounds; ++round) {
+        SP_CNT(14);
         for (int j = SP_TID; j < n; j += SP_NT) L.hv[j] = G.cc[j] == 0 ? 1.0 / (G.pp[j] + reg) : 0.0;
         for (int i = SP_TID; i < m; i += SP_NT) G.rdg[i] = G.rc[i] ? reg : -1.0;
         SP_SYNC();
@@ -841,6 +876,7 @@ PHX_HD int sp_rounds(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds&
                 L.hv[j] = r1 / (G.pp[j] + reg);
             }
             SP_SYNC();
+            SP_TP(3);
             sp_rows(P, Y, s, L.xv, L.hv, [&](int i, double ax, double adr) {
                 const int rc = G.rc[i];
                 if (!rc) { L.tv[i] = 0.0; return; }
@@ -848,6 +884,7 @@ PHX_HD int sp_rounds(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds&
                 L.tv[i] = adr - (b - ax);
             });
             SP_SYNC();
+            SP_TP(4);
             sp_msolve(P, Y, L);
             double mx[2] = {0.0, 0.0};   // max |correction|, max |value|
             for (int j = SP_TID; j < n; j += SP_NT) {
@@ -872,6 +909,8 @@ PHX_HD int sp_rounds(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds&
             sp_reduce<2>(mx, L.red, 1);
             if (SP_TID == 0 && refine_total) ++*refine_total;
             SP_SYNC();
+            SP_TP(6);
+            SP_CNT(12);
             if (mx[0] <= 1e-10 * (1.0 + mx[1])) break;
         }
         // ---- certificate; keeps the multipliers (r1) and row activities (ax) ----
@@ -907,6 +946,7 @@ PHX_HD int sp_rounds(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds&
             }
         });
         sp_reduce<1>(bad, L.red, 1);
+        SP_TP(7);
         if (bad[0] == 0.0) return round + 1;
         if (round + 1 == rounds) break;
         SP_SYNC();
@@ -933,6 +973,7 @@ PHX_HD int sp_rounds(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds&
             else if (r == 0 && ax > bu && (ax - bu) / dr > ptol * (1.0 + fabs(bu / dr))) G.rc[i] = 2;
         }
         SP_SYNC();
+        SP_TP(8);
     }
     return 0;
 }

@@ -88,5 +88,10 @@ case "$1" in
           "bench:r05_s23_c2:--only C2 $A" "bench:r05_s23_c5a:--only C5a $A" && \
        PHX_WG_BLK=0 $J "bench:r05_s23_c5a_blk0:--only C5a $A" && \
        PHX_WG_PROF=1 $J "bench:r05_s23_c2_wgprof:--only C2 $A" && PHX_WG_BLK=0 PHX_WG_PROF=1 $J "bench:r05_s23_c5a_blk0_wgprof:--only C5a $A" ;;
+  s24) # sparse solver phase clocks (PHX_SP_PROF): C5b (Iter0 interior point + warm rounds), C5a; C2 workgroup round budget 4 / 6 against 8
+       $J "test:tests/test_netdes.py tests/test_sslp.py" && \
+       PHX_SP_PROF=1 $J "bench:r05_s24_c5b_spprof:--only C5b $A" "bench:r05_s24_c5a_spprof:--only C5a $A" && \
+       $J "bench:r05_s24_c2_w4:--only C2 $A --so {\"wg_warm\":4,\"wg_first\":1}" "bench:r05_s24_c2_w6:--only C2 $A --so {\"wg_warm\":6,\"wg_first\":1}" \
+          "bench:r05_s24_c2:--only C2 $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
