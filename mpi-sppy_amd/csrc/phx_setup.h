@@ -5,6 +5,7 @@
 // entries stay invariant after scaling).  Shared by phx_kernels.hip and the
 // test-only CPU emulation (tests/emu).
 #pragma once
+#include <limits>
 #include <stdint.h>
 #include <math.h>
 #include <string>
@@ -159,6 +160,41 @@ struct SpSymHost {
     int nC = 0, nlink = 0;
     std::vector<int32_t> cpos, crow, lptr, lc, lrow, lkp, lkb, lkc, clp, cll, eap, eka, ekb, ebp, el1, el2;
 };
+
+// The sparse solver's gather tables (round 5), from the symbolic structure and
+// the scaled constant A (hs.Acs): per separator-Schur direct term t the product
+// A[eka] A[ekb] (NaN when either entry varies by scenario) and the shared
+// column; per link term the same for A[lkb] A[lkc]; A's values and variation
+// indices in CSC order.  Each replaces a chain of dependent global loads
+// (position -> kvar -> value, position -> column) in the factor's assembly and
+// the column loops by loads that only depend on the loop index.
+struct SpTablesHost {
+    std::vector<double> eab, lab, Acsc;
+    std::vector<int32_t> ecol, lcol, kvcsc;
+};
+inline void build_sp_tables(const HostSetup& hs, const SpSymHost& h, SpTablesHost& t) {
+    const double nan = std::numeric_limits<double>::quiet_NaN();
+    const auto prod = [&](int ka, int kb) {
+        return (hs.kvar[ka] < 0 && hs.kvar[kb] < 0) ? hs.Acs[ka] * hs.Acs[kb] : nan;
+    };
+    t = SpTablesHost{};
+    for (size_t q = 0; q < h.eka.size(); ++q) {
+        t.eab.push_back(prod(h.eka[q], h.ekb[q]));
+        t.ecol.push_back(hs.colidx[h.eka[q]]);
+    }
+    for (size_t q = 0; q < h.lkb.size(); ++q) {
+        t.lab.push_back(prod(h.lkb[q], h.lkc[q]));
+        t.lcol.push_back(hs.colidx[h.lkb[q]]);
+    }
+    for (size_t k = 0; k < hs.csc2csr.size(); ++k) {
+        t.Acsc.push_back(hs.Acs[hs.csc2csr[k]]);
+        t.kvcsc.push_back(hs.kvar[hs.csc2csr[k]]);
+    }
+    // (non-empty, so that their data pointers are valid)
+    if (t.eab.empty()) { t.eab.push_back(0.0); t.ecol.push_back(0); }
+    if (t.lab.empty()) { t.lab.push_back(0.0); t.lcol.push_back(0); }
+    if (t.Acsc.empty()) { t.Acsc.push_back(0.0); t.kvcsc.push_back(-1); }
+}
 
 inline bool build_sp_sym(const HostSetup& hs, int n, int m, int max_c, SpSymHost& out, std::string& why) {
     out = SpSymHost{};

@@ -103,6 +103,13 @@ struct SpSym {
     const int32_t* el1;    //   link of a B row into c1
     const int32_t* el2;    //   link of the same B row into c2
     const double* AvT;     // [S][nvar] scaled scenario-varying A values, scenario-major
+    // gather tables (phx_setup.h build_sp_tables)
+    const double* eab;     // [eap[nC*nC]] A[eka] A[ekb] of a direct term, NaN: either varies
+    const int32_t* ecol;   //   its column
+    const double* lab;     // [lkp[nlink]] A[lkb] A[lkc] of a link term, NaN: either varies
+    const int32_t* lcol;   //   its column
+    const double* Acsc;    // [nnz] scaled constant A in CSC order
+    const int32_t* kvcsc;  // [nnz] its variation index (-1: constant) in CSC order
 };
 
 // One scenario's LDS.
@@ -200,9 +207,20 @@ PHX_HD SpScr sp_scr_carve(double* base, int n, int m) {
     return G;
 }
 
+// (branch-free: the constant value, the variation index and -- at a clamped
+// index -- the scenario's value are loaded without waiting for each other)
 PHX_HD double sp_a(const Prob& P, const SpSym& Y, int k, int s) {
     const int v = P.kvar[k];
-    return v < 0 ? P.Ac[k] : Y.AvT[(int64_t)s * Y.nvar + v];
+    const double ac = P.Ac[k];
+    const double av = Y.AvT[(int64_t)s * Y.nvar + (v < 0 ? 0 : v)];
+    return v < 0 ? ac : av;
+}
+// A at CSC position k (the column loops), without the csc2csr hop
+PHX_HD double sp_a_csc(const SpSym& Y, int k, int s) {
+    const int v = Y.kvcsc[k];
+    const double ac = Y.Acsc[k];
+    const double av = Y.AvT[(int64_t)s * Y.nvar + (v < 0 ? 0 : v)];
+    return v < 0 ? ac : av;
 }
 
 // A row phase: body(i, (A v1)_i, (A v2)_i) for every row i, the B rows by a
@@ -300,8 +318,8 @@ PHX_HD bool sp_factor_once(const Prob& P, const SpSym& Y, const SpScr& G, const 
             double w = 0.0;
             if (rd >= 0.0 && G.rdg[Y.crow[Y.lc[l]]] >= 0.0)
                 for (int t = Y.lkp[l]; t < Y.lkp[l + 1]; ++t) {
-                    const int kb = Y.lkb[t];
-                    w += sp_a(P, Y, kb, s) * sp_a(P, Y, Y.lkc[t], s) * L.hv[P.colidx[kb]];
+                    const double ab = Y.lab[t];
+                    w += (ab == ab ? ab : sp_a(P, Y, Y.lkb[t], s) * sp_a(P, Y, Y.lkc[t], s)) * L.hv[Y.lcol[t]];
                 }
             L.lv[l] = w;
         }
@@ -318,8 +336,8 @@ PHX_HD bool sp_factor_once(const Prob& P, const SpSym& Y, const SpScr& G, const 
         double v = 0.0;
         if (!(d1 < 0.0 || d2 < 0.0)) {
             for (int t = Y.eap[p]; t < Y.eap[p + 1]; ++t) {
-                const int ka = Y.eka[t];
-                v += sp_a(P, Y, ka, s) * sp_a(P, Y, Y.ekb[t], s) * L.hv[P.colidx[ka]];
+                const double ab = Y.eab[t];
+                v += (ab == ab ? ab : sp_a(P, Y, Y.eka[t], s) * sp_a(P, Y, Y.ekb[t], s)) * L.hv[Y.ecol[t]];
             }
             for (int t = Y.ebp[p]; t < Y.ebp[p + 1]; ++t) {
                 const int l1 = Y.el1[t];
@@ -337,8 +355,8 @@ PHX_HD bool sp_factor_once(const Prob& P, const SpSym& Y, const SpScr& G, const 
         }
         double v = 0.0, w = 0.0;
         for (int t = Y.eap[p] + SP_QL; t < Y.eap[p + 1]; t += SP_QW) {
-            const int ka = Y.eka[t];
-            v += sp_a(P, Y, ka, s) * sp_a(P, Y, Y.ekb[t], s) * L.hv[P.colidx[ka]];
+            const double ab = Y.eab[t];
+            v += (ab == ab ? ab : sp_a(P, Y, Y.eka[t], s) * sp_a(P, Y, Y.ekb[t], s)) * L.hv[Y.ecol[t]];
         }
         for (int t = Y.ebp[p] + SP_QL; t < Y.ebp[p + 1]; t += SP_QW) {
             const int l1 = Y.el1[t];
@@ -539,7 +557,7 @@ PHX_HD double sp_kkt_error(const Prob& P, const SpSym& Y, const SpScr& G, const 
     for (int j = SP_TID; j < P.n; j += SP_NT) {
         double aty = 0.0;
         for (int k = P.colptr[j]; k < P.colptr[j + 1]; ++k)
-            aty += sp_a(P, Y, P.csc2csr[k], s) * L.yv[P.rowidx[k]];
+            aty += sp_a_csc(Y, k, s) * L.yv[P.rowidx[k]];
         G.aty[j] = aty;
         const double q = G.qq[j], p = G.pp[j], x = L.xv[j];
         const double lam_s = q + p * x - aty;
@@ -621,7 +639,7 @@ PHX_HD void sp_direction(const Prob& P, const SpSym& Y, const SpScr& G, const Sp
         if (l == u) continue;
         double atdy = 0.0;
         for (int k = P.colptr[j]; k < P.colptr[j + 1]; ++k)
-            atdy += sp_a(P, Y, P.csc2csr[k], s) * L.tv[P.rowidx[k]];
+            atdy += sp_a_csc(Y, k, s) * L.tv[P.rowidx[k]];
         const double dxv = (G.dx[j] + atdy) / G.hx[j];
         G.dx[j] = dxv;
         if (isfinite(l)) G.dzl[j] = (G.cl[j] - G.zl[j] * dxv) / (x - l);
@@ -826,7 +844,7 @@ PHX_HD void sp_classify(const Prob& P, const SpSym& Y, const SpScr& G, const SpL
         const double x = L.xv[j], l = G.lb[j], u = G.ub[j];
         double aty = 0.0;
         for (int k = P.colptr[j]; k < P.colptr[j + 1]; ++k)
-            aty += sp_a(P, Y, P.csc2csr[k], s) * L.yv[P.rowidx[k]];
+            aty += sp_a_csc(Y, k, s) * L.yv[P.rowidx[k]];
         const double lam = G.qq[j] + G.pp[j] * x - aty;
         int c = 0;
         if (isfinite(l) && (x - l <= tol * (1.0 + fabs(l)) || x - l < lam)) c = 1;
@@ -870,7 +888,7 @@ PHX_HD int sp_rounds(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds&
                 if (G.cc[j]) { G.r1[j] = 0.0; L.hv[j] = 0.0; continue; }
                 double atz = 0.0;
                 for (int k = P.colptr[j]; k < P.colptr[j + 1]; ++k)
-                    atz += sp_a(P, Y, P.csc2csr[k], s) * L.yv[P.rowidx[k]];
+                    atz += sp_a_csc(Y, k, s) * L.yv[P.rowidx[k]];
                 const double r1 = -G.qq[j] - G.pp[j] * L.xv[j] - atz;
                 G.r1[j] = r1;
                 L.hv[j] = r1 / (G.pp[j] + reg);
@@ -891,7 +909,7 @@ PHX_HD int sp_rounds(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds&
                 if (G.cc[j]) continue;
                 double atz = 0.0;
                 for (int k = P.colptr[j]; k < P.colptr[j + 1]; ++k)
-                    atz += sp_a(P, Y, P.csc2csr[k], s) * L.tv[P.rowidx[k]];
+                    atz += sp_a_csc(Y, k, s) * L.tv[P.rowidx[k]];
                 const double dx = (G.r1[j] - atz) / (G.pp[j] + reg);
                 const double x = L.xv[j] + dx;
                 L.xv[j] = x;
@@ -921,7 +939,7 @@ PHX_HD int sp_rounds(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds&
             if (x > u && (x - u) * dc > ptol * (1.0 + fabs(u * dc))) bad[0] = 1.0;
             double atz = 0.0;
             for (int k = P.colptr[j]; k < P.colptr[j + 1]; ++k)
-                atz += sp_a(P, Y, P.csc2csr[k], s) * L.yv[P.rowidx[k]];
+                atz += sp_a_csc(Y, k, s) * L.yv[P.rowidx[k]];
             const double lam = (G.qq[j] + G.pp[j] * x + atz) / dc;
             G.r1[j] = lam;
             if (!(lam - lam == 0.0)) bad[0] = 1.0;   // non-finite x or y: no comparison would fail
@@ -990,7 +1008,7 @@ PHX_HD bool sp_farkas(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds
     for (int j = SP_TID; j < P.n; j += SP_NT) {
         double g = 0.0;
         for (int k = P.colptr[j]; k < P.colptr[j + 1]; ++k)
-            g += sp_a(P, Y, P.csc2csr[k], s) * L.yv[P.rowidx[k]] * iy;
+            g += sp_a_csc(Y, k, s) * L.yv[P.rowidx[k]] * iy;
         farkas_col(F, g, G.lb[j], G.ub[j]);
     }
     for (int i = SP_TID; i < P.m; i += SP_NT) farkas_row(F, L.yv[i] * iy, G.bl[i], G.bu[i]);

@@ -93,5 +93,9 @@ case "$1" in
        PHX_SP_PROF=1 $J "bench:r05_s24_c5b_spprof:--only C5b $A" "bench:r05_s24_c5a_spprof:--only C5a $A" && \
        $J "bench:r05_s24_c2_w4:--only C2 $A --so {\"wg_warm\":4,\"wg_first\":1}" "bench:r05_s24_c2_w6:--only C2 $A --so {\"wg_warm\":6,\"wg_first\":1}" \
           "bench:r05_s24_c2:--only C2 $A" ;;
+  s25) # sparse solver gather tables (constant term products, CSC-ordered A) + branch-free A loads: parity, C5b / C5a / C2, C5b phase clocks
+       $J "test:tests/test_netdes.py tests/test_sslp.py tests/test_bench_settings.py tests/test_gpu_parity.py" \
+          "bench:r05_s25_c5b:--only C5b $A" "bench:r05_s25_c5a:--only C5a $A" "bench:r05_s25_c2:--only C2 $A" && \
+       PHX_SP_PROF=1 $J "bench:r05_s25_c5b_spprof:--only C5b $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
