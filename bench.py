@@ -304,7 +304,8 @@ def workloads():
                    # the workgroup pass's round budget: the lanes that need more
                    # go on to the sparse interior point either way (measured,
                    # r04_s31/s32: 16 rounds 0.98-0.99 ms per step, 8 0.94-0.95,
-                   # 6 0.92, 4 2.76 -- eight stops instead of one); in the first
+                   # 6 0.92, 4 2.76 -- eight stops instead of one; r05_s24, the
+                   # in-stream sparse step: 8 0.604, 6 0.602, 4 1.88); in the first
                    # PH iteration after Iter0 the pass certifies almost no lane
                    # (emulation, 300 scenarios: 12 of 300 with 8 rounds), so one
                    # round there (wg_first) before the interior point
@@ -314,6 +315,11 @@ def workloads():
                    kw=lambda S, cm: {"branching_factors": bfs}, S=1000,
                    nodes=sputils.create_nodenames_from_branching_factors(bfs),
                    desc="aircond branching 10x10x10, 1,000 scenarios, 111 non-leaf nodes (BASELINE configs[3])",
+                   # every timed launch bracketed (the unfused loop's default samples
+                   # every fifth: two of ten, and C4's launches range 25-190 us with
+                   # the early iterations' rescue rounds -- r04 verdict): the average
+                   # is the timed window's, as a kernel trace's
+                   so={"iterk_timing": -1},
                    cpu=dict(model="aircond", scens=1000, iters=4, total=1000)),
         "C5a": dict(creator=sslp.scenario_creator, names=lambda S: sslp.scenario_names_creator(10000),
                     kw=lambda S, cm: {"num_scens": 10000}, nodes=None, S=10000,

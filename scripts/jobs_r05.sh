@@ -97,5 +97,8 @@ case "$1" in
        $J "test:tests/test_netdes.py tests/test_sslp.py tests/test_bench_settings.py tests/test_gpu_parity.py" \
           "bench:r05_s25_c5b:--only C5b $A" "bench:r05_s25_c5a:--only C5a $A" "bench:r05_s25_c2:--only C2 $A" && \
        PHX_SP_PROF=1 $J "bench:r05_s25_c5b_spprof:--only C5b $A" ;;
+  s26) # C4 with every timed launch bracketed; C5a workgroup round budget 6 / 8 against 4
+       $J "bench:r05_s26_c4:--only C4 $A" "bench:r05_s26_c5a:--only C5a $A" \
+          "bench:r05_s26_c5a_w6:--only C5a $A --so {\"wg_warm\":6}" "bench:r05_s26_c5a_w8:--only C5a $A --so {\"wg_warm\":8}" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
