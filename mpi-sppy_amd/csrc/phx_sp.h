@@ -154,19 +154,22 @@ struct SpLds {
 // hv, xv: nlink + m + 2n doubles) live in the workgroup's global scratch slot
 // instead of LDS, so that more workgroups fit a CU (netdes 50-30-H: 129 KB of
 // LDS per workgroup, one per CU, against 46 KB, three).
-PHX_HD size_t sp_split_doubles(int n, int m, int nlink) {
-    return (size_t)nlink + (size_t)m + 2 * (size_t)n;
+// Level 2 (round 5): the row right-hand side / solution tv too (netdes: 46 ->
+// 34 KB of LDS, four workgroups per CU with k_sp_solve_t<4>'s register cap).
+PHX_HD size_t sp_split_doubles(int n, int m, int nlink, int level = 1) {
+    return (size_t)nlink + (size_t)m + 2 * (size_t)n + (level >= 2 ? (size_t)m : 0);
 }
 
-PHX_HD size_t sp_lds_bytes(int n, int m, int nC, int nlink, bool split = false) {
+PHX_HD size_t sp_lds_bytes(int n, int m, int nC, int nlink, int split = 0) {
     const size_t ld = (size_t)(nC | 1);
     size_t d = (size_t)nC * ld + 2 * (size_t)nC + 2 * (size_t)m + 8 * SP_RED;
     if (!split) d += sp_split_doubles(n, m, nlink);
+    if (split >= 2) d -= (size_t)m;
     return d * 8;
 }
 
-// gbase: the split vectors' place (null: LDS, after the rest)
-PHX_HD SpLds sp_carve(double* base, int n, int m, int nC, int nlink, double* gbase = nullptr) {
+// gbase: the split vectors' place (null: LDS, after the rest); level 2: tv there too
+PHX_HD SpLds sp_carve(double* base, int n, int m, int nC, int nlink, double* gbase = nullptr, int level = 1) {
     SpLds L;
     double* d = base;
     L.red = d; d += 8 * SP_RED;
@@ -174,8 +177,10 @@ PHX_HD SpLds sp_carve(double* base, int n, int m, int nC, int nlink, double* gba
     L.dg = d; d += nC;
     L.cv = d; d += nC;
     L.yv = d; d += m;
-    L.tv = d; d += m;
+    const bool tvg = gbase && level >= 2;
+    if (!tvg) { L.tv = d; d += m; }
     double* g = gbase ? gbase : d;
+    if (tvg) { L.tv = g; g += m; }
     L.lv = g; g += nlink;
     L.Mbb = g; g += m;
     L.hv = g; g += n;

@@ -100,5 +100,8 @@ case "$1" in
   s26) # C4 with every timed launch bracketed; C5a workgroup round budget 6 / 8 against 4
        $J "bench:r05_s26_c4:--only C4 $A" "bench:r05_s26_c5a:--only C5a $A" \
           "bench:r05_s26_c5a_w6:--only C5a $A --so {\"wg_warm\":6}" "bench:r05_s26_c5a_w8:--only C5a $A --so {\"wg_warm\":8}" ;;
+  s27) # the sparse solver's split level 2 (tv in the slot too: four workgroups per CU with the capped kernel) on C5b: parity, time
+       PHX_SP_SPLIT=2 $J "test:tests/test_netdes.py" "bench:r05_s27_c5b_split2:--only C5b $A" && \
+       $J "bench:r05_s27_c5b:--only C5b $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
