@@ -103,5 +103,19 @@ case "$1" in
   s27) # the sparse solver's split level 2 (tv in the slot too: four workgroups per CU with the capped kernel) on C5b: parity, time
        PHX_SP_SPLIT=2 $J "test:tests/test_netdes.py" "bench:r05_s27_c5b_split2:--only C5b $A" && \
        $J "bench:r05_s27_c5b:--only C5b $A" ;;
+  final) # the round's evidence: the whole GPU suite, the driver's default command, kernel traces
+       $J "test:tests" && $J "bench:r05_final_default:--detail gpurun_out/r05_final_default_detail.json" \
+          "prof:r05_final_prof:$H --ar-probe 0" "prof:r05_final_c3s8_prof:$S8" "prof:r05_final_1m_prof:$M" \
+          "prof:r05_final_c2_prof:--only C2 $A" "prof:r05_final_c4_prof:--only C4 $A" "prof:r05_final_c5a_prof:--only C5a $A" \
+          "prof:r05_final_c5b_prof:--only C5b $A" ;;
+  pmc1) # PMC passes on the final kernels (one counter group per pass): the lane kernels
+       $J "pmc:r05_pmc_c3_fetch:FETCH_SIZE:$B" "pmc:r05_pmc_c3_write:WRITE_SIZE:$B" "pmc:r05_pmc_c3_sq:$SQ:$B" \
+          "pmc:r05_pmc_s8_fetch:FETCH_SIZE:$S8" "pmc:r05_pmc_s8_write:WRITE_SIZE:$S8" "pmc:r05_pmc_s8_sq:$SQ:$S8" \
+          "pmc:r05_pmc_1m_fetch:FETCH_SIZE:$M" "pmc:r05_pmc_1m_write:WRITE_SIZE:$M" \
+          "pmc:r05_pmc_c4_fetch:FETCH_SIZE:--only C4 $A" "pmc:r05_pmc_c4_write:WRITE_SIZE:--only C4 $A" ;;
+  pmc2) # ... the workgroup and sparse solvers
+       $J "pmc:r05_pmc_c2_fetch:FETCH_SIZE:--only C2 $A" "pmc:r05_pmc_c2_write:WRITE_SIZE:--only C2 $A" \
+          "pmc:r05_pmc_c5a_fetch:FETCH_SIZE:--only C5a $A" "pmc:r05_pmc_c5a_write:WRITE_SIZE:--only C5a $A" \
+          "pmc:r05_pmc_c5b_fetch:FETCH_SIZE:--only C5b $A" "pmc:r05_pmc_c5b_write:WRITE_SIZE:--only C5b $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac

@@ -485,27 +485,33 @@ def test_deferred_iter0_gpu(gpu_lib, so0):
         assert a.solve_stats[0]["stragglers"] > 0
 
 
-@pytest.mark.parametrize("env,creator_kw", [
-    ("PHX_WG_SPLIT", ("farmer", {"num_scens": 300, "crops_multiplier": 10})),
-    ("PHX_SP_SPLIT", ("sslp", {"num_scens": 64})),
+@pytest.mark.parametrize("env,creator_kw,levels", [
+    # farmer cm=10: A varies (the split area holds A's values, the pattern is shared)
+    ("PHX_WG_SPLIT", ("farmer", {"num_scens": 300, "crops_multiplier": 10}), ("0", "1")),
+    # sslp: A constant (pattern and A shared by every workgroup; the default layout)
+    ("PHX_WG_SPLIT", ("sslp", {"num_scens": 64}), ("0", "1")),
+    # level 2: the row vector in the scratch slot too
+    ("PHX_SP_SPLIT", ("sslp", {"num_scens": 64}), ("0", "1", "2")),
 ])
-def test_split_layouts_bit_equal_gpu(gpu_lib, monkeypatch, env, creator_kw):
+def test_split_layouts_bit_equal_gpu(gpu_lib, monkeypatch, env, creator_kw, levels):
     """The workgroup / sparse solvers' split layouts (per-scenario vectors in a
-    global area instead of LDS: phx_wg.h / phx_sp.h) move memory, not arithmetic:
-    the same PH trajectory bit for bit as the all-LDS layout."""
+    global area instead of LDS, scenario-invariant arrays shared: phx_wg.h /
+    phx_sp.h) move memory, not arithmetic: the same PH trajectory bit for bit as
+    the all-LDS layout."""
     from mpisppy_amd.examples import sslp
     mod = farmer if creator_kw[0] == "farmer" else sslp
     kw = creator_kw[1]
     names = mod.scenario_names_creator(kw["num_scens"])
     out = {}
-    for v in ("0", "1"):
+    for v in levels:
         monkeypatch.setenv(env, v)
         ph, conv, E, tb = run_engine(mod.scenario_creator, names, kw, 3, lib=gpu_lib)
         assert all_certified(ph)
         out[v] = (ph.W_array(), ph.xbar_by_node()["ROOT"][0], E, tb)
-    assert np.array_equal(out["0"][0], out["1"][0])
-    assert np.array_equal(out["0"][1], out["1"][1])
-    assert out["0"][2] == out["1"][2] and out["0"][3] == out["1"][3]
+    for v in levels[1:]:
+        assert np.array_equal(out[levels[0]][0], out[v][0]), v
+        assert np.array_equal(out[levels[0]][1], out[v][1]), v
+        assert out[levels[0]][2] == out[v][2] and out[levels[0]][3] == out[v][3], v
 
 
 def test_window_timing_fused_loop_gpu(gpu_lib):
