@@ -117,5 +117,12 @@ case "$1" in
        $J "pmc:r05_pmc_c2_fetch:FETCH_SIZE:--only C2 $A" "pmc:r05_pmc_c2_write:WRITE_SIZE:--only C2 $A" \
           "pmc:r05_pmc_c5a_fetch:FETCH_SIZE:--only C5a $A" "pmc:r05_pmc_c5a_write:WRITE_SIZE:--only C5a $A" \
           "pmc:r05_pmc_c5b_fetch:FETCH_SIZE:--only C5b $A" "pmc:r05_pmc_c5b_write:WRITE_SIZE:--only C5b $A" ;;
+  s28) # the workgroup pass's leftovers (the in-stream sparse interior point): C5a / C2 round budgets with single-change
+       # rounds after a few full ones (PHX_WG_SINGLE_AFTER), sparse phase clocks for the leftovers' interior-point counts
+       PHX_SP_PROF=1 $J "bench:r05_s28_c5a:--only C5a $A" "bench:r05_s28_c5a_w8:--only C5a $A --so {\"wg_warm\":8}" \
+          "bench:r05_s28_c2:--only C2 $A" && \
+       PHX_SP_PROF=1 PHX_WG_SINGLE_AFTER=4 $J "bench:r05_s28_c5a_w8_sa4:--only C5a $A --so {\"wg_warm\":8}" \
+          "bench:r05_s28_c5a_w16_sa4:--only C5a $A --so {\"wg_warm\":16}" "bench:r05_s28_c2_sa4:--only C2 $A" \
+          "bench:r05_s28_c2_w16_sa4:--only C2 $A --so {\"wg_warm\":16,\"wg_first\":1}" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
