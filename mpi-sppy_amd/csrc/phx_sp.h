@@ -230,10 +230,13 @@ PHX_HD double sp_a_csc(const SpSym& Y, int k, int s) {
 
 // A row phase: body(i, (A v1)_i, (A v2)_i) for every row i, the B rows by a
 // thread each, the separator rows by a quad each (every thread of the quad
-// computes the sums; body runs on the quad's first).  v2 null: 0.
+// computes the sums; body runs on the quad's first) -- every row by a quad when
+// there are at most as many rows as quads (sslp: 60 rows, its 45 client rows
+// 15 entries each).  v2 null: 0.
 template <class F>
 PHX_HD void sp_rows(const Prob& P, const SpSym& Y, int s, const double* v1, const double* v2, F&& body) {
-    for (int i = SP_TID; i < P.m; i += SP_NT) {
+    const bool allq = P.m <= SP_QN && SP_QW > 1;
+    for (int i = SP_TID; i < (allq ? 0 : P.m); i += SP_NT) {
         if (Y.cpos[i] >= 0) continue;
         double a1 = 0.0, a2 = 0.0;
         for (int k = P.rowptr[i]; k < P.rowptr[i + 1]; ++k) {
@@ -244,8 +247,8 @@ PHX_HD void sp_rows(const Prob& P, const SpSym& Y, int s, const double* v1, cons
         }
         body(i, a1, a2);
     }
-    for (int c = SP_QID; c < Y.nC; c += SP_QN) {
-        const int i = Y.crow[c];
+    for (int c = SP_QID; c < (allq ? P.m : Y.nC); c += SP_QN) {
+        const int i = allq ? c : Y.crow[c];
         double a1 = 0.0, a2 = 0.0;
         for (int k = P.rowptr[i] + SP_QL; k < P.rowptr[i + 1]; k += SP_QW) {
             const double a = sp_a(P, Y, k, s);
@@ -306,20 +309,26 @@ PHX_HD bool sp_factor(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds
 PHX_HD bool sp_factor_once(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds& L, int s,
                            bool ipm_safe) {
     const int m = P.m, nC = Y.nC, ld = Y.ld;
-    // B-row diagonal and the links M_bc
-    for (int i = SP_TID; i < m; i += SP_NT) {
+    // B-row diagonal and the links M_bc (a quad per B row when there are at
+    // most as many rows as quads, as sp_rows: its entries and its links
+    // interleaved)
+    const bool bq = m <= SP_QN && SP_QW > 1;
+    const int b_id = bq ? SP_QID : SP_TID, b_n = bq ? SP_QN : SP_NT, b_l = bq ? SP_QL : 0, b_w = bq ? SP_QW : 1;
+    for (int i = b_id; i < m; i += b_n) {
         if (Y.cpos[i] >= 0) continue;
         const double rd = G.rdg[i];
         double v = 1.0;
         if (rd >= 0.0) {
-            v = rd;
-            for (int k = P.rowptr[i]; k < P.rowptr[i + 1]; ++k) {
+            double t = 0.0;
+            for (int k = P.rowptr[i] + b_l; k < P.rowptr[i + 1]; k += b_w) {
                 const double a = sp_a(P, Y, k, s);
-                v += a * a * L.hv[P.colidx[k]];
+                t += a * a * L.hv[P.colidx[k]];
             }
+            if (bq) t = sp_quad_sum(t);
+            v = rd + t;
         }
-        L.Mbb[i] = v;
-        for (int l = Y.lptr[i]; l < Y.lptr[i + 1]; ++l) {
+        if (b_l == 0) L.Mbb[i] = v;
+        for (int l = Y.lptr[i] + b_l; l < Y.lptr[i + 1]; l += b_w) {
             double w = 0.0;
             if (rd >= 0.0 && G.rdg[Y.crow[Y.lc[l]]] >= 0.0)
                 for (int t = Y.lkp[l]; t < Y.lkp[l + 1]; ++t) {
@@ -334,22 +343,30 @@ PHX_HD bool sp_factor_once(const Prob& P, const SpSym& Y, const SpScr& G, const 
     // off-diagonal entries a thread each (a few terms: the columns and B rows
     // two separator rows share), the diagonal ones a quad each (every column
     // and B row of the row: netdes ~60 + ~30 terms)
-    for (int p = SP_TID; p < nC * nC; p += SP_NT) {
+    // (a quad each too when there are at most twice as many entries as quads:
+    // sslp's 105 each sum over all 45 client rows)
+    const bool offq = nC * (nC - 1) / 2 <= 2 * SP_QN && SP_QW > 1;
+    const int o_id = offq ? SP_QID : SP_TID, o_n = offq ? SP_QN : SP_NT, o_l = offq ? SP_QL : 0, o_w = offq ? SP_QW : 1;
+    for (int p = o_id; p < nC * nC; p += o_n) {
         const int c1 = p / nC, c2 = p - c1 * nC;
         if (c2 >= c1) continue;
         const double d1 = G.rdg[Y.crow[c1]], d2 = G.rdg[Y.crow[c2]];
-        double v = 0.0;
+        double v = 0.0, w = 0.0;
         if (!(d1 < 0.0 || d2 < 0.0)) {
-            for (int t = Y.eap[p]; t < Y.eap[p + 1]; ++t) {
+            for (int t = Y.eap[p] + o_l; t < Y.eap[p + 1]; t += o_w) {
                 const double ab = Y.eab[t];
                 v += (ab == ab ? ab : sp_a(P, Y, Y.eka[t], s) * sp_a(P, Y, Y.ekb[t], s)) * L.hv[Y.ecol[t]];
             }
-            for (int t = Y.ebp[p]; t < Y.ebp[p + 1]; ++t) {
+            for (int t = Y.ebp[p] + o_l; t < Y.ebp[p + 1]; t += o_w) {
                 const int l1 = Y.el1[t];
-                v -= L.lv[l1] * L.lv[Y.el2[t]] / L.Mbb[Y.lrow[l1]];
+                w += L.lv[l1] * L.lv[Y.el2[t]] / L.Mbb[Y.lrow[l1]];
             }
         }
-        L.Sm[c1 * ld + c2] = v;
+        if (offq) {
+            v = sp_quad_sum(v);
+            w = sp_quad_sum(w);
+        }
+        if (o_l == 0) L.Sm[c1 * ld + c2] = v - w;
     }
     for (int c = SP_QID; c < nC; c += SP_QN) {
         const int p = c * nC + c;

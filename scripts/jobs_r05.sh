@@ -124,5 +124,9 @@ case "$1" in
        PHX_SP_PROF=1 PHX_WG_SINGLE_AFTER=4 $J "bench:r05_s28_c5a_w8_sa4:--only C5a $A --so {\"wg_warm\":8}" \
           "bench:r05_s28_c5a_w16_sa4:--only C5a $A --so {\"wg_warm\":16}" "bench:r05_s28_c2_sa4:--only C2 $A" \
           "bench:r05_s28_c2_w16_sa4:--only C2 $A --so {\"wg_warm\":16,\"wg_first\":1}" ;;
+  s29) # sparse solver, small problems (sslp): every row / off-diagonal Schur entry / B row a quad -- parity, C5a / C5b / C2, clocks
+       $J "test:tests/test_sslp.py tests/test_netdes.py tests/test_bench_settings.py tests/test_trajectories.py tests/test_gpu_parity.py" \
+          "bench:r05_s29_c5a:--only C5a $A" "bench:r05_s29_c5b:--only C5b $A" "bench:r05_s29_c2:--only C2 $A" && \
+       PHX_SP_PROF=1 $J "bench:r05_s29_c5a_spprof:--only C5a $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
