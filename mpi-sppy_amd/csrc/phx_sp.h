@@ -118,7 +118,8 @@ struct SpLds {
     double *dg;    // [nC] 1 / L_kk
     double *cv;    // [nC] separator right-hand side / solution
     double *lv;    // [nlink] M_bc of each link
-    double *Mbb;   // [m] diagonal of M on the B rows
+    double *Mbb;   // [m] 1 / (the diagonal of M) on the B rows (one division per B row per
+                   //     factorisation; the Schur terms and the M solves multiply)
     double *hv;    // [n] column weights H^-1 / gathered column vector
     double *xv;    // [n] x (scaled)
     double *yv;    // [m] y (interior point) or z = -y (active set)
@@ -327,7 +328,7 @@ PHX_HD bool sp_factor_once(const Prob& P, const SpSym& Y, const SpScr& G, const 
             if (bq) t = sp_quad_sum(t);
             v = rd + t;
         }
-        if (b_l == 0) L.Mbb[i] = v;
+        if (b_l == 0) L.Mbb[i] = 1.0 / v;
         for (int l = Y.lptr[i] + b_l; l < Y.lptr[i + 1]; l += b_w) {
             double w = 0.0;
             if (rd >= 0.0 && G.rdg[Y.crow[Y.lc[l]]] >= 0.0)
@@ -359,7 +360,7 @@ PHX_HD bool sp_factor_once(const Prob& P, const SpSym& Y, const SpScr& G, const 
             }
             for (int t = Y.ebp[p] + o_l; t < Y.ebp[p + 1]; t += o_w) {
                 const int l1 = Y.el1[t];
-                w += L.lv[l1] * L.lv[Y.el2[t]] / L.Mbb[Y.lrow[l1]];
+                w += L.lv[l1] * L.lv[Y.el2[t]] * L.Mbb[Y.lrow[l1]];
             }
         }
         if (offq) {
@@ -382,7 +383,7 @@ PHX_HD bool sp_factor_once(const Prob& P, const SpSym& Y, const SpScr& G, const 
         }
         for (int t = Y.ebp[p] + SP_QL; t < Y.ebp[p + 1]; t += SP_QW) {
             const int l1 = Y.el1[t];
-            w += L.lv[l1] * L.lv[Y.el2[t]] / L.Mbb[Y.lrow[l1]];
+            w += L.lv[l1] * L.lv[Y.el2[t]] * L.Mbb[Y.lrow[l1]];
         }
         v = d1 + sp_quad_sum(v);
         w = sp_quad_sum(w);
@@ -517,7 +518,7 @@ PHX_HD void sp_msolve(const Prob& P, const SpSym& Y, const SpLds& L) {
         for (int q = Y.clp[c] + SP_QL; q < Y.clp[c + 1]; q += SP_QW) {
             const int l = Y.cll[q];
             const int b = Y.lrow[l];
-            v += L.lv[l] * L.tv[b] / L.Mbb[b];
+            v += L.lv[l] * L.tv[b] * L.Mbb[b];
         }
         v = sp_quad_sum(v);
         if (SP_QL == 0) L.cv[c] = L.tv[Y.crow[c]] - v;
@@ -529,7 +530,7 @@ PHX_HD void sp_msolve(const Prob& P, const SpSym& Y, const SpLds& L) {
         if (c >= 0) { L.tv[i] = L.cv[c]; continue; }
         double v = L.tv[i];
         for (int l = Y.lptr[i]; l < Y.lptr[i + 1]; ++l) v -= L.lv[l] * L.cv[Y.lc[l]];
-        L.tv[i] = v / L.Mbb[i];
+        L.tv[i] = v * L.Mbb[i];
     }
     SP_SYNC();
     SP_TP(5);
