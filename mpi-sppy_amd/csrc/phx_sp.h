@@ -72,14 +72,6 @@ namespace phx {
 #define SP_QID 0
 #define SP_QN 1
 #endif
-// Gather loops (a term's indices, then the values they point at): unrolled by
-// four on the device so that four terms' loads are in flight at once (the
-// loops carry only their sum)
-#if defined(__HIP_DEVICE_COMPILE__)
-#define SP_UNROLL4 _Pragma("unroll 4")
-#else
-#define SP_UNROLL4
-#endif
 PHX_HD double sp_quad_sum(double v) {
 #if defined(__HIP_DEVICE_COMPILE__)
     v += __shfl_xor(v, 1, 64);
@@ -362,12 +354,10 @@ PHX_HD bool sp_factor_once(const Prob& P, const SpSym& Y, const SpScr& G, const 
         const double d1 = G.rdg[Y.crow[c1]], d2 = G.rdg[Y.crow[c2]];
         double v = 0.0, w = 0.0;
         if (!(d1 < 0.0 || d2 < 0.0)) {
-            SP_UNROLL4
             for (int t = Y.eap[p] + o_l; t < Y.eap[p + 1]; t += o_w) {
                 const double ab = Y.eab[t];
                 v += (ab == ab ? ab : sp_a(P, Y, Y.eka[t], s) * sp_a(P, Y, Y.ekb[t], s)) * L.hv[Y.ecol[t]];
             }
-            SP_UNROLL4
             for (int t = Y.ebp[p] + o_l; t < Y.ebp[p + 1]; t += o_w) {
                 const int l1 = Y.el1[t];
                 w += L.lv[l1] * L.lv[Y.el2[t]] * L.Mbb[Y.lrow[l1]];
@@ -387,12 +377,10 @@ PHX_HD bool sp_factor_once(const Prob& P, const SpSym& Y, const SpScr& G, const 
             continue;
         }
         double v = 0.0, w = 0.0;
-        SP_UNROLL4
         for (int t = Y.eap[p] + SP_QL; t < Y.eap[p + 1]; t += SP_QW) {
             const double ab = Y.eab[t];
             v += (ab == ab ? ab : sp_a(P, Y, Y.eka[t], s) * sp_a(P, Y, Y.ekb[t], s)) * L.hv[Y.ecol[t]];
         }
-        SP_UNROLL4
         for (int t = Y.ebp[p] + SP_QL; t < Y.ebp[p + 1]; t += SP_QW) {
             const int l1 = Y.el1[t];
             w += L.lv[l1] * L.lv[Y.el2[t]] * L.Mbb[Y.lrow[l1]];
