@@ -132,5 +132,8 @@ case "$1" in
        $J "test:tests/test_sslp.py tests/test_netdes.py tests/test_bench_settings.py tests/test_trajectories.py tests/test_gpu_parity.py" \
           "bench:r05_s30_c5a:--only C5a $A" "bench:r05_s30_c5b:--only C5b $A" && \
        PHX_SP_PROF=1 $J "bench:r05_s30_c5a_spprof:--only C5a $A" ;;
+  s31) # (measured and reverted) the separator Schur term loops unrolled by four -- C5a / C5b, clocks
+       $J "bench:r05_s31_c5a:--only C5a $A" "bench:r05_s31_c5b:--only C5b $A" && \
+       PHX_SP_PROF=1 $J "bench:r05_s31_c5a_spprof:--only C5a $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
