@@ -135,5 +135,9 @@ case "$1" in
   s31) # (measured and reverted) the separator Schur term loops unrolled by four -- C5a / C5b, clocks
        $J "bench:r05_s31_c5a:--only C5a $A" "bench:r05_s31_c5b:--only C5b $A" && \
        PHX_SP_PROF=1 $J "bench:r05_s31_c5a_spprof:--only C5a $A" ;;
+  s32) # headline solver-option sweep (same box): as_rounds 3 / 5 / 6 against 4, iterk depth 8, seed templates 32
+       $J "bench:r05_s32_h:$H" "bench:r05_s32_h_as3:$H --so {\"as_rounds\":3}" "bench:r05_s32_h_as5:$H --so {\"as_rounds\":5}" \
+          "bench:r05_s32_h_as6:$H --so {\"as_rounds\":6}" "bench:r05_s32_h_d8:$H --depth 8" \
+          "bench:r05_s32_h_t32:$H --so {\"seed_templates\":32}" "bench:r05_s32_h2:$H" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
