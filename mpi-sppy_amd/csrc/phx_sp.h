@@ -200,14 +200,18 @@ PHX_HD size_t sp_scr_doubles(int n, int m) {
     return 14 * (size_t)n + 12 * (size_t)m + ((size_t)n + (size_t)m + 1) / 2 + 2;
 }
 
-PHX_HD SpScr sp_scr_carve(double* base, int n, int m) {
+// rows_lds: the twelve row vectors' place when they fit the workgroup's LDS
+// (small problems: sslp, 60 rows -- 5.8 KB; null: in the slot)
+PHX_HD SpScr sp_scr_carve(double* base, int n, int m, double* rows_lds = nullptr) {
     SpScr G;
     double* d = base;
     double** cols[] = {&G.qq, &G.pp, &G.lb, &G.ub, &G.r1, &G.aty, &G.dx, &G.zl, &G.zu, &G.dzl, &G.dzu,
                        &G.cl, &G.cu, &G.hx};
     for (double** p : cols) { *p = d; d += n; }
     double** rows[] = {&G.bl, &G.bu, &G.ax, &G.rdg, &G.s, &G.wl, &G.wu, &G.ds, &G.dwl, &G.dwu, &G.cwl, &G.cwu};
-    for (double** p : rows) { *p = d; d += m; }
+    double* r = rows_lds ? rows_lds : d;
+    for (double** p : rows) { *p = r; r += m; }
+    if (!rows_lds) d = r;
     G.cc = (int32_t*)d;
     G.rc = G.cc + n;
     return G;

@@ -139,5 +139,9 @@ case "$1" in
        $J "bench:r05_s32_h:$H" "bench:r05_s32_h_as3:$H --so {\"as_rounds\":3}" "bench:r05_s32_h_as5:$H --so {\"as_rounds\":5}" \
           "bench:r05_s32_h_as6:$H --so {\"as_rounds\":6}" "bench:r05_s32_h_d8:$H --depth 8" \
           "bench:r05_s32_h_t32:$H --so {\"seed_templates\":32}" "bench:r05_s32_h2:$H" ;;
+  s33) # the sparse scratch's row vectors in LDS (small problems): parity (incl. bit equality), C5a / C5b / C2, clocks
+       $J "test:tests/test_sslp.py tests/test_netdes.py tests/test_bench_settings.py tests/test_trajectories.py tests/test_gpu_parity.py" \
+          "bench:r05_s33_c5a:--only C5a $A" "bench:r05_s33_c5b:--only C5b $A" "bench:r05_s33_c2:--only C2 $A" && \
+       PHX_SP_PROF=1 $J "bench:r05_s33_c5a_spprof:--only C5a $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac

@@ -492,6 +492,8 @@ def test_deferred_iter0_gpu(gpu_lib, so0):
     ("PHX_WG_SPLIT", ("sslp", {"num_scens": 64}), ("0", "1")),
     # level 2: the row vector in the scratch slot too
     ("PHX_SP_SPLIT", ("sslp", {"num_scens": 64}), ("0", "1", "2")),
+    # the sparse scratch's row vectors in LDS (the default where they fit) or in the slot
+    ("PHX_SP_ROWS_LDS", ("sslp", {"num_scens": 64}), ("1", "0")),
 ])
 def test_split_layouts_bit_equal_gpu(gpu_lib, monkeypatch, env, creator_kw, levels):
     """The workgroup / sparse solvers' split layouts (per-scenario vectors in a
