@@ -219,6 +219,17 @@ PHX_HD SpScr sp_scr_carve(double* base, int n, int m, double* rows_lds = nullptr
 
 // (branch-free: the constant value, the variation index and -- at a clamped
 // index -- the scenario's value are loaded without waiting for each other)
+// Column bounds the same in every scenario (no per-scenario fixing): the
+// scratch's lb / ub point at the problem's shared arrays (L2-resident, read by
+// every workgroup) instead of a per-slot copy re-read from memory
+PHX_HD SpScr sp_scr_shared(SpScr G, const Prob& P) {
+    if (P.lb.ss == 0 && P.lb.si == 1 && P.ub.ss == 0 && P.ub.si == 1) {
+        G.lb = (double*)P.lb.p;      // (never written: sp_load skips them)
+        G.ub = (double*)P.ub.p;
+    }
+    return G;
+}
+
 PHX_HD double sp_a(const Prob& P, const SpSym& Y, int k, int s) {
     const int v = P.kvar[k];
     const double ac = P.Ac[k];
@@ -551,8 +562,10 @@ PHX_HD double sp_load(const Prob& P, const SpScr& G, const SpLds& L, int s) {
         col_cost(P, j, s, q, p);
         G.qq[j] = q;
         G.pp[j] = p;
-        G.lb[j] = P.lb.at(j, s);
-        G.ub[j] = P.ub.at(j, s);
+        if (G.lb != P.lb.p) {
+            G.lb[j] = P.lb.at(j, s);
+            G.ub[j] = P.ub.at(j, s);
+        }
         qm = fmax(qm, fabs(q / P.dc[j]));
     }
     for (int i = SP_TID; i < P.m; i += SP_NT) {

@@ -143,5 +143,8 @@ case "$1" in
        $J "test:tests/test_sslp.py tests/test_netdes.py tests/test_bench_settings.py tests/test_trajectories.py tests/test_gpu_parity.py" \
           "bench:r05_s33_c5a:--only C5a $A" "bench:r05_s33_c5b:--only C5b $A" "bench:r05_s33_c2:--only C2 $A" && \
        PHX_SP_PROF=1 $J "bench:r05_s33_c5a_spprof:--only C5a $A" ;;
+  s34) # the sparse scratch's column bounds shared when scenario-invariant: parity, C5a / C5b / C2
+       $J "test:tests/test_sslp.py tests/test_netdes.py tests/test_bench_settings.py tests/test_trajectories.py tests/test_gpu_parity.py" \
+          "bench:r05_s34_c5a:--only C5a $A" "bench:r05_s34_c5b:--only C5b $A" "bench:r05_s34_c2:--only C2 $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
