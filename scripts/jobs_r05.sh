@@ -146,5 +146,11 @@ case "$1" in
   s34) # the sparse scratch's column bounds shared when scenario-invariant: parity, C5a / C5b / C2
        $J "test:tests/test_sslp.py tests/test_netdes.py tests/test_bench_settings.py tests/test_trajectories.py tests/test_gpu_parity.py" \
           "bench:r05_s34_c5a:--only C5a $A" "bench:r05_s34_c5b:--only C5b $A" "bench:r05_s34_c2:--only C2 $A" ;;
+  s35) # C5a: single-change workgroup rounds early (PHX_WG_SINGLE_AFTER) with larger budgets, against the default
+       PHX_SP_PROF=1 $J "bench:r05_s35_c5a:--only C5a $A" && \
+       PHX_SP_PROF=1 PHX_WG_SINGLE_AFTER=1 $J "bench:r05_s35_c5a_sa1_w16:--only C5a $A --so {\"wg_warm\":16}" \
+          "bench:r05_s35_c5a_sa1_w32:--only C5a $A --so {\"wg_warm\":32}" && \
+       PHX_SP_PROF=1 PHX_WG_SINGLE_AFTER=2 $J "bench:r05_s35_c5a_sa2_w16:--only C5a $A --so {\"wg_warm\":16}" && \
+       PHX_SP_PROF=1 PHX_WG_SINGLE_AFTER=3 $J "bench:r05_s35_c5a_sa3_w24:--only C5a $A --so {\"wg_warm\":24}" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
