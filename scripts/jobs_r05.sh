@@ -152,5 +152,8 @@ case "$1" in
           "bench:r05_s35_c5a_sa1_w32:--only C5a $A --so {\"wg_warm\":32}" && \
        PHX_SP_PROF=1 PHX_WG_SINGLE_AFTER=2 $J "bench:r05_s35_c5a_sa2_w16:--only C5a $A --so {\"wg_warm\":16}" && \
        PHX_SP_PROF=1 PHX_WG_SINGLE_AFTER=3 $J "bench:r05_s35_c5a_sa3_w24:--only C5a $A --so {\"wg_warm\":24}" ;;
+  s36) # C4: the single-change rule (JIT defines): the multiplier first / the primal violation first, against the larger of the two
+       $J "bench:r05_s36_c4:--only C4 $A" && PHX_LANE_DEFS="PHX_SINGLE_DUAL_FIRST" $J "bench:r05_s36_c4_dual:--only C4 $A" && \
+       PHX_LANE_DEFS="PHX_SINGLE_PRIMAL_FIRST" $J "bench:r05_s36_c4_primal:--only C4 $A" && $J "bench:r05_s36_c4b:--only C4 $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
