@@ -723,41 +723,15 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
             // fly with the very expressions the one-pivot step would store
             // (row k col b: Sm[k][b] - (Sm[k][a] / d_a) * Sm[b][a]), so the
             // factor is the same; half the barriers and row round trips
-            // Round 5: the next pair's pivot quantities (the same expressions)
-            // are formed during this step by thread 0, whose wavefront updates
-            // rows a+2 and a+3 first, into a double buffer (L.t / L.u: free
-            // until the refinement), so a step starts with one LDS read instead
-            // of the divide / square-root chain on every thread
-            const bool pipe = m >= 8;
-            double* const pbuf[2] = {L.t, L.u};
-            const auto piv_compute = [&](int a, double* bf) {
-                const double d0 = L.Sm[a * ld + a];
-                const double e = L.Sm[(a + 1) * ld + a], id0 = 1.0 / d0;
-                const double d1 = L.Sm[(a + 1) * ld + a + 1] - (e * id0) * e;
-                bf[0] = d0; bf[1] = e; bf[2] = id0; bf[3] = d1;
-                bf[4] = sqrt(d0); bf[5] = sqrt(d1); bf[6] = 1.0 / d1;
-            };
-            if (pipe) {
-                if (WG_TID == 0 && ma >= 2) piv_compute(0, pbuf[0]);
-                WG_SYNC();
-            }
-            int j2 = 0, par = 0;
-            for (; j2 + 1 < ma; j2 += 2, par ^= 1) {
+            int j2 = 0;
+            for (; j2 + 1 < ma; j2 += 2) {
                 const int a = j2, b = j2 + 1;
-                double d0, e, id0, d1, sd0, sd1, id1;
-                if (pipe) {
-                    const double* bf = pbuf[par];
-                    d0 = bf[0]; e = bf[1]; id0 = bf[2]; d1 = bf[3]; sd0 = bf[4]; sd1 = bf[5]; id1 = bf[6];
-                    if (!(d0 > 0.0)) { spd = false; break; }
-                    if (!(d1 > 0.0)) { spd = false; break; }
-                } else {
-                    d0 = L.Sm[a * ld + a];
-                    if (!(d0 > 0.0)) { spd = false; break; }
-                    e = L.Sm[b * ld + a]; id0 = 1.0 / d0;
-                    d1 = L.Sm[b * ld + b] - (e * id0) * e;
-                    if (!(d1 > 0.0)) { spd = false; break; }
-                    sd0 = sqrt(d0); sd1 = sqrt(d1); id1 = 1.0 / d1;
-                }
+                const double d0 = L.Sm[a * ld + a];
+                if (!(d0 > 0.0)) { spd = false; break; }
+                const double e = L.Sm[b * ld + a], id0 = 1.0 / d0;
+                const double d1 = L.Sm[b * ld + b] - (e * id0) * e;
+                if (!(d1 > 0.0)) { spd = false; break; }
+                const double sd0 = sqrt(d0), sd1 = sqrt(d1), id1 = 1.0 / d1;
                 for (int i = b + 1 + WG_QID; i < ma; i += WG_QN) {
                     double* row = L.Sm + (size_t)i * ld;
                     const double lia = row[a];
@@ -776,8 +750,6 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
                         L.Sm[b * ld + i] = lib / sd1;
                     }
                 }
-                // (rows a+2, a+3 are quads 0 and 1 of thread 0's wavefront: final here)
-                if (pipe && WG_TID == 0 && j2 + 3 < ma) piv_compute(j2 + 2, pbuf[par ^ 1]);
                 if (WG_TID == 0) {
                     L.dg[a] = 1.0 / sd0;
                     L.dg[b] = 1.0 / sd1;
