@@ -155,5 +155,9 @@ case "$1" in
   s36) # C4: the single-change rule (JIT defines): the multiplier first / the primal violation first, against the larger of the two
        $J "bench:r05_s36_c4:--only C4 $A" && PHX_LANE_DEFS="PHX_SINGLE_DUAL_FIRST" $J "bench:r05_s36_c4_dual:--only C4 $A" && \
        PHX_LANE_DEFS="PHX_SINGLE_PRIMAL_FIRST" $J "bench:r05_s36_c4_primal:--only C4 $A" && $J "bench:r05_s36_c4b:--only C4 $A" ;;
+  s37) # (measured and reverted) the pivot pairs' divide / square-root chain formed one step ahead -- parity, C2 / C5a, clocks
+       $J "test:tests/test_sslp.py tests/test_bench_settings.py tests/test_trajectories.py tests/test_gpu_parity.py" \
+          "bench:r05_s37_c2:--only C2 $A" "bench:r05_s37_c5a:--only C5a $A" && \
+       PHX_WG_PROF=1 $J "bench:r05_s37_c2_wgprof:--only C2 $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
