@@ -627,15 +627,20 @@ PHX_HD double sp_kkt_error(const Prob& P, const SpSym& Y, const SpScr& G, const 
 // the normal matrix solved by sp_factor / sp_msolve.
 // ---------------------------------------------------------------------------
 PHX_HD void sp_direction(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds& L, int s) {
+    // (the interior point's column / row loops load everything they may use
+    // before their branches: one memory round trip per element instead of a
+    // chain of them; the arithmetic is unchanged)
     for (int j = SP_TID; j < P.n; j += SP_NT) {
         const double l = G.lb[j], u = G.ub[j], x = L.xv[j];
+        const double pp = G.pp[j], qq = G.qq[j], aty = G.aty[j], zl = G.zl[j], zu = G.zu[j], cl = G.cl[j],
+                     cu = G.cu[j], hx = G.hx[j];
         if (l == u) { G.dx[j] = 0.0; L.hv[j] = 0.0; continue; }
-        double rd = G.pp[j] * x + G.qq[j] - G.aty[j];
+        double rd = pp * x + qq - aty;
         double rho = 0.0;
-        if (isfinite(l)) { rd -= G.zl[j]; rho += G.cl[j] / (x - l); }
-        if (isfinite(u)) { rd += G.zu[j]; rho -= G.cu[j] / (u - x); }
+        if (isfinite(l)) { rd -= zl; rho += cl / (x - l); }
+        if (isfinite(u)) { rd += zu; rho -= cu / (u - x); }
         G.dx[j] = rho - rd;
-        L.hv[j] = (rho - rd) / G.hx[j];
+        L.hv[j] = (rho - rd) / hx;
     }
     SP_SYNC();
     sp_rows(P, Y, s, L.hv, nullptr, [&](int i, double adr, double) {
@@ -650,9 +655,10 @@ PHX_HD void sp_direction(const Prob& P, const SpSym& Y, const SpScr& G, const Sp
             G.ds[i] = 0.0;
         } else {
             const double sv = G.s[i], y = L.yv[i];
+            const double wl = G.wl[i], wu = G.wu[i], cwl = G.cwl[i], cwu = G.cwu[i];
             double rs = y, rhos = 0.0, sig = 0.0;
-            if (isfinite(bl)) { rs -= G.wl[i]; rhos += G.cwl[i] / (sv - bl); sig += G.wl[i] / (sv - bl); }
-            if (isfinite(bu)) { rs += G.wu[i]; rhos -= G.cwu[i] / (bu - sv); sig += G.wu[i] / (bu - sv); }
+            if (isfinite(bl)) { rs -= wl; rhos += cwl / (sv - bl); sig += wl / (sv - bl); }
+            if (isfinite(bu)) { rs += wu; rhos -= cwu / (bu - sv); sig += wu / (bu - sv); }
             rhos -= rs;
             G.ds[i] = rhos;
             rhs = -(ax - sv) + rhos / sig - adr;
@@ -664,26 +670,28 @@ PHX_HD void sp_direction(const Prob& P, const SpSym& Y, const SpScr& G, const Sp
     sp_msolve(P, Y, L);
     for (int i = SP_TID; i < P.m; i += SP_NT) {
         const double bl = G.bl[i], bu = G.bu[i];
+        const double dy = L.tv[i], sv = G.s[i], wl = G.wl[i], wu = G.wu[i], ds = G.ds[i], cwl = G.cwl[i],
+                     cwu = G.cwu[i];
         if (bl == bu || (!isfinite(bl) && !isfinite(bu))) continue;
-        const double dy = L.tv[i], sv = G.s[i];
         double sig = 0.0;
-        if (isfinite(bl)) sig += G.wl[i] / (sv - bl);
-        if (isfinite(bu)) sig += G.wu[i] / (bu - sv);
-        const double dsv = (G.ds[i] - dy) / sig;
+        if (isfinite(bl)) sig += wl / (sv - bl);
+        if (isfinite(bu)) sig += wu / (bu - sv);
+        const double dsv = (ds - dy) / sig;
         G.ds[i] = dsv;
-        if (isfinite(bl)) G.dwl[i] = (G.cwl[i] - G.wl[i] * dsv) / (sv - bl);
-        if (isfinite(bu)) G.dwu[i] = (G.cwu[i] + G.wu[i] * dsv) / (bu - sv);
+        if (isfinite(bl)) G.dwl[i] = (cwl - wl * dsv) / (sv - bl);
+        if (isfinite(bu)) G.dwu[i] = (cwu + wu * dsv) / (bu - sv);
     }
     for (int j = SP_TID; j < P.n; j += SP_NT) {
         const double l = G.lb[j], u = G.ub[j], x = L.xv[j];
+        const double dx = G.dx[j], hx = G.hx[j], cl = G.cl[j], zl = G.zl[j], cu = G.cu[j], zu = G.zu[j];
         if (l == u) continue;
         double atdy = 0.0;
         for (int k = P.colptr[j]; k < P.colptr[j + 1]; ++k)
             atdy += sp_a_csc(Y, k, s) * L.tv[P.rowidx[k]];
-        const double dxv = (G.dx[j] + atdy) / G.hx[j];
+        const double dxv = (dx + atdy) / hx;
         G.dx[j] = dxv;
-        if (isfinite(l)) G.dzl[j] = (G.cl[j] - G.zl[j] * dxv) / (x - l);
-        if (isfinite(u)) G.dzu[j] = (G.cu[j] + G.zu[j] * dxv) / (u - x);
+        if (isfinite(l)) G.dzl[j] = (cl - zl * dxv) / (x - l);
+        if (isfinite(u)) G.dzu[j] = (cu + zu * dxv) / (u - x);
     }
     SP_TP(11);
 }
@@ -692,26 +700,28 @@ PHX_HD void sp_steps(const Prob& P, const SpScr& G, const SpLds& L, double& ap, 
     double v[2] = {1.0, 1.0};
     for (int j = SP_TID; j < P.n; j += SP_NT) {
         const double l = G.lb[j], u = G.ub[j], x = L.xv[j], d = G.dx[j];
+        const double dzl = G.dzl[j], zl = G.zl[j], dzu = G.dzu[j], zu = G.zu[j];
         if (l == u) continue;
         if (isfinite(l)) {
             if (d < 0.0) v[0] = fmin(v[0], -(x - l) / d);
-            if (G.dzl[j] < 0.0) v[1] = fmin(v[1], -G.zl[j] / G.dzl[j]);
+            if (dzl < 0.0) v[1] = fmin(v[1], -zl / dzl);
         }
         if (isfinite(u)) {
             if (d > 0.0) v[0] = fmin(v[0], (u - x) / d);
-            if (G.dzu[j] < 0.0) v[1] = fmin(v[1], -G.zu[j] / G.dzu[j]);
+            if (dzu < 0.0) v[1] = fmin(v[1], -zu / dzu);
         }
     }
     for (int i = SP_TID; i < P.m; i += SP_NT) {
         const double bl = G.bl[i], bu = G.bu[i], sv = G.s[i], d = G.ds[i];
+        const double dwl = G.dwl[i], wl = G.wl[i], dwu = G.dwu[i], wu = G.wu[i];
         if (bl == bu) continue;
         if (isfinite(bl)) {
             if (d < 0.0) v[0] = fmin(v[0], -(sv - bl) / d);
-            if (G.dwl[i] < 0.0) v[1] = fmin(v[1], -G.wl[i] / G.dwl[i]);
+            if (dwl < 0.0) v[1] = fmin(v[1], -wl / dwl);
         }
         if (isfinite(bu)) {
             if (d > 0.0) v[0] = fmin(v[0], (bu - sv) / d);
-            if (G.dwu[i] < 0.0) v[1] = fmin(v[1], -G.wu[i] / G.dwu[i]);
+            if (dwu < 0.0) v[1] = fmin(v[1], -wu / dwu);
         }
     }
     sp_reduce<2>(v, L.red, 2);
@@ -756,16 +766,16 @@ PHX_HD double sp_ipm(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds&
         err = sp_kkt_error(P, Y, G, L, s);
         double mu_acc[2] = {0.0, 0.0};
         for (int j = SP_TID; j < n; j += SP_NT) {
-            const double l = G.lb[j], u = G.ub[j], x = L.xv[j];
+            const double l = G.lb[j], u = G.ub[j], x = L.xv[j], zl = G.zl[j], zu = G.zu[j];
             if (l == u) continue;
-            if (isfinite(l)) { mu_acc[0] += (x - l) * G.zl[j]; mu_acc[1] += 1.0; }
-            if (isfinite(u)) { mu_acc[0] += (u - x) * G.zu[j]; mu_acc[1] += 1.0; }
+            if (isfinite(l)) { mu_acc[0] += (x - l) * zl; mu_acc[1] += 1.0; }
+            if (isfinite(u)) { mu_acc[0] += (u - x) * zu; mu_acc[1] += 1.0; }
         }
         for (int i = SP_TID; i < m; i += SP_NT) {
-            const double bl = G.bl[i], bu = G.bu[i], sv = G.s[i];
+            const double bl = G.bl[i], bu = G.bu[i], sv = G.s[i], wl = G.wl[i], wu = G.wu[i];
             if (bl == bu) continue;
-            if (isfinite(bl)) { mu_acc[0] += (sv - bl) * G.wl[i]; mu_acc[1] += 1.0; }
-            if (isfinite(bu)) { mu_acc[0] += (bu - sv) * G.wu[i]; mu_acc[1] += 1.0; }
+            if (isfinite(bl)) { mu_acc[0] += (sv - bl) * wl; mu_acc[1] += 1.0; }
+            if (isfinite(bu)) { mu_acc[0] += (bu - sv) * wu; mu_acc[1] += 1.0; }
         }
         sp_reduce<2>(mu_acc, L.red, 0);
         SP_TP(9);
@@ -775,12 +785,12 @@ PHX_HD double sp_ipm(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds&
         if (err < tol || !(err < 1e300)) break;
         // column weights H^-1 and row diagonals of the normal matrix
         for (int j = SP_TID; j < n; j += SP_NT) {
-            const double l = G.lb[j], u = G.ub[j], x = L.xv[j];
+            const double l = G.lb[j], u = G.ub[j], x = L.xv[j], zl = G.zl[j], zu = G.zu[j];
             double h = G.pp[j] + reg;
             if (l == u) h = 1e300;
             else {
-                if (isfinite(l)) h += G.zl[j] / (x - l);
-                if (isfinite(u)) h += G.zu[j] / (u - x);
+                if (isfinite(l)) h += zl / (x - l);
+                if (isfinite(u)) h += zu / (u - x);
             }
             G.hx[j] = h;
             L.hv[j] = (l == u) ? 0.0 : 1.0 / h;
@@ -791,10 +801,10 @@ PHX_HD double sp_ipm(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds&
             if (!isfinite(bl) && !isfinite(bu)) dg = -1.0;
             else if (bl == bu) dg = reg;
             else {
-                const double sv = G.s[i];
+                const double sv = G.s[i], wl = G.wl[i], wu = G.wu[i];
                 double sig = 0.0;
-                if (isfinite(bl)) sig += G.wl[i] / (sv - bl);
-                if (isfinite(bu)) sig += G.wu[i] / (bu - sv);
+                if (isfinite(bl)) sig += wl / (sv - bl);
+                if (isfinite(bu)) sig += wu / (bu - sv);
                 dg = 1.0 / sig + reg;
             }
             G.rdg[i] = dg;
@@ -803,14 +813,14 @@ PHX_HD double sp_ipm(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds&
         if (!sp_factor(P, Y, G, L, s, true)) break;
         // ---- predictor ----
         for (int j = SP_TID; j < n; j += SP_NT) {
-            const double l = G.lb[j], u = G.ub[j], x = L.xv[j];
-            G.cl[j] = isfinite(l) ? -(x - l) * G.zl[j] : 0.0;
-            G.cu[j] = isfinite(u) ? -(u - x) * G.zu[j] : 0.0;
+            const double l = G.lb[j], u = G.ub[j], x = L.xv[j], zl = G.zl[j], zu = G.zu[j];
+            G.cl[j] = isfinite(l) ? -(x - l) * zl : 0.0;
+            G.cu[j] = isfinite(u) ? -(u - x) * zu : 0.0;
         }
         for (int i = SP_TID; i < m; i += SP_NT) {
-            const double bl = G.bl[i], bu = G.bu[i], sv = G.s[i];
-            G.cwl[i] = (isfinite(bl) && bl != bu) ? -(sv - bl) * G.wl[i] : 0.0;
-            G.cwu[i] = (isfinite(bu) && bl != bu) ? -(bu - sv) * G.wu[i] : 0.0;
+            const double bl = G.bl[i], bu = G.bu[i], sv = G.s[i], wl = G.wl[i], wu = G.wu[i];
+            G.cwl[i] = (isfinite(bl) && bl != bu) ? -(sv - bl) * wl : 0.0;
+            G.cwu[i] = (isfinite(bu) && bl != bu) ? -(bu - sv) * wu : 0.0;
         }
         sp_direction(P, Y, G, L, s);
         double ap, ad;
@@ -818,15 +828,17 @@ PHX_HD double sp_ipm(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds&
         double maff[1] = {0.0};
         for (int j = SP_TID; j < n; j += SP_NT) {
             const double l = G.lb[j], u = G.ub[j], x = L.xv[j];
+            const double dx = G.dx[j], zl = G.zl[j], dzl = G.dzl[j], zu = G.zu[j], dzu = G.dzu[j];
             if (l == u) continue;
-            if (isfinite(l)) maff[0] += (x - l + ap * G.dx[j]) * (G.zl[j] + ad * G.dzl[j]);
-            if (isfinite(u)) maff[0] += (u - x - ap * G.dx[j]) * (G.zu[j] + ad * G.dzu[j]);
+            if (isfinite(l)) maff[0] += (x - l + ap * dx) * (zl + ad * dzl);
+            if (isfinite(u)) maff[0] += (u - x - ap * dx) * (zu + ad * dzu);
         }
         for (int i = SP_TID; i < m; i += SP_NT) {
             const double bl = G.bl[i], bu = G.bu[i], sv = G.s[i];
+            const double ds = G.ds[i], wl = G.wl[i], dwl = G.dwl[i], wu = G.wu[i], dwu = G.dwu[i];
             if (bl == bu) continue;
-            if (isfinite(bl)) maff[0] += (sv - bl + ap * G.ds[i]) * (G.wl[i] + ad * G.dwl[i]);
-            if (isfinite(bu)) maff[0] += (bu - sv - ap * G.ds[i]) * (G.wu[i] + ad * G.dwu[i]);
+            if (isfinite(bl)) maff[0] += (sv - bl + ap * ds) * (wl + ad * dwl);
+            if (isfinite(bu)) maff[0] += (bu - sv - ap * ds) * (wu + ad * dwu);
         }
         sp_reduce<1>(maff, L.red, 0);
         const double ma = ncomp > 0.0 ? maff[0] / ncomp : 0.0;
@@ -835,13 +847,15 @@ PHX_HD double sp_ipm(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds&
         // ---- corrector ----
         for (int j = SP_TID; j < n; j += SP_NT) {
             const double l = G.lb[j], u = G.ub[j], x = L.xv[j];
-            G.cl[j] = isfinite(l) ? smu - (x - l) * G.zl[j] - G.dx[j] * G.dzl[j] : 0.0;
-            G.cu[j] = isfinite(u) ? smu - (u - x) * G.zu[j] + G.dx[j] * G.dzu[j] : 0.0;
+            const double dx = G.dx[j], zl = G.zl[j], dzl = G.dzl[j], zu = G.zu[j], dzu = G.dzu[j];
+            G.cl[j] = isfinite(l) ? smu - (x - l) * zl - dx * dzl : 0.0;
+            G.cu[j] = isfinite(u) ? smu - (u - x) * zu + dx * dzu : 0.0;
         }
         for (int i = SP_TID; i < m; i += SP_NT) {
             const double bl = G.bl[i], bu = G.bu[i], sv = G.s[i];
-            G.cwl[i] = (isfinite(bl) && bl != bu) ? smu - (sv - bl) * G.wl[i] - G.ds[i] * G.dwl[i] : 0.0;
-            G.cwu[i] = (isfinite(bu) && bl != bu) ? smu - (bu - sv) * G.wu[i] + G.ds[i] * G.dwu[i] : 0.0;
+            const double ds = G.ds[i], wl = G.wl[i], dwl = G.dwl[i], wu = G.wu[i], dwu = G.dwu[i];
+            G.cwl[i] = (isfinite(bl) && bl != bu) ? smu - (sv - bl) * wl - ds * dwl : 0.0;
+            G.cwu[i] = (isfinite(bu) && bl != bu) ? smu - (bu - sv) * wu + ds * dwu : 0.0;
         }
         SP_SYNC();
         sp_direction(P, Y, G, L, s);

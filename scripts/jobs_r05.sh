@@ -159,5 +159,9 @@ case "$1" in
        $J "test:tests/test_sslp.py tests/test_bench_settings.py tests/test_trajectories.py tests/test_gpu_parity.py" \
           "bench:r05_s37_c2:--only C2 $A" "bench:r05_s37_c5a:--only C5a $A" && \
        PHX_WG_PROF=1 $J "bench:r05_s37_c2_wgprof:--only C2 $A" ;;
+  s38) # the sparse interior point's loops with their loads ahead of the branches: parity, C5a / C5b / C2, clocks
+       $J "test:tests/test_sslp.py tests/test_netdes.py tests/test_bench_settings.py tests/test_trajectories.py tests/test_gpu_parity.py" \
+          "bench:r05_s38_c5a:--only C5a $A" "bench:r05_s38_c5b:--only C5b $A" "bench:r05_s38_c2:--only C2 $A" && \
+       PHX_SP_PROF=1 $J "bench:r05_s38_c5a_spprof:--only C5a $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
