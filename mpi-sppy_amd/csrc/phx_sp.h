@@ -595,15 +595,13 @@ PHX_HD double sp_kkt_error(const Prob& P, const SpSym& Y, const SpScr& G, const 
         else if (y < 0.0 && isfinite(bu)) acc[5] += bu * y;
     });
     for (int j = SP_TID; j < P.n; j += SP_NT) {
+        const double q = G.qq[j], p = G.pp[j], x = L.xv[j], dc = P.dc[j], l = G.lb[j], u = G.ub[j];
         double aty = 0.0;
         for (int k = P.colptr[j]; k < P.colptr[j + 1]; ++k)
             aty += sp_a_csc(Y, k, s) * L.yv[P.rowidx[k]];
         G.aty[j] = aty;
-        const double q = G.qq[j], p = G.pp[j], x = L.xv[j];
         const double lam_s = q + p * x - aty;
-        const double dc = P.dc[j];
         const double lam = lam_s / dc;
-        const double l = G.lb[j], u = G.ub[j];
         double rd = lam;
         if (isfinite(l) && lam > 0.0) { rd = 0.0; acc[5] += l * lam_s; }
         if (isfinite(u) && lam < 0.0) { rd = 0.0; acc[5] += u * lam_s; }
@@ -895,11 +893,11 @@ PHX_HD double sp_ipm(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds&
 // ---------------------------------------------------------------------------
 PHX_HD void sp_classify(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds& L, int s, double tol) {
     for (int j = SP_TID; j < P.n; j += SP_NT) {
-        const double x = L.xv[j], l = G.lb[j], u = G.ub[j];
+        const double x = L.xv[j], l = G.lb[j], u = G.ub[j], qq = G.qq[j], pp = G.pp[j];
         double aty = 0.0;
         for (int k = P.colptr[j]; k < P.colptr[j + 1]; ++k)
             aty += sp_a_csc(Y, k, s) * L.yv[P.rowidx[k]];
-        const double lam = G.qq[j] + G.pp[j] * x - aty;
+        const double lam = qq + pp * x - aty;
         int c = 0;
         if (isfinite(l) && (x - l <= tol * (1.0 + fabs(l)) || x - l < lam)) c = 1;
         else if (isfinite(u) && (u - x <= tol * (1.0 + fabs(u)) || u - x < -lam)) c = 2;
@@ -939,13 +937,15 @@ PHX_HD int sp_rounds(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds&
         // ---- iterative refinement on the unregularised KKT (proximal point) ----
         for (int it = 0; it < O.refine_steps; ++it) {
             for (int j = SP_TID; j < n; j += SP_NT) {
-                if (G.cc[j]) { G.r1[j] = 0.0; L.hv[j] = 0.0; continue; }
+                const int cc = G.cc[j];
+                const double qq = G.qq[j], pp = G.pp[j], xj = L.xv[j];
+                if (cc) { G.r1[j] = 0.0; L.hv[j] = 0.0; continue; }
                 double atz = 0.0;
                 for (int k = P.colptr[j]; k < P.colptr[j + 1]; ++k)
                     atz += sp_a_csc(Y, k, s) * L.yv[P.rowidx[k]];
-                const double r1 = -G.qq[j] - G.pp[j] * L.xv[j] - atz;
+                const double r1 = -qq - pp * xj - atz;
                 G.r1[j] = r1;
-                L.hv[j] = r1 / (G.pp[j] + reg);
+                L.hv[j] = r1 / (pp + reg);
             }
             SP_SYNC();
             SP_TP(3);
@@ -960,20 +960,23 @@ PHX_HD int sp_rounds(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds&
             sp_msolve(P, Y, L);
             double mx[2] = {0.0, 0.0};   // max |correction|, max |value|
             for (int j = SP_TID; j < n; j += SP_NT) {
-                if (G.cc[j]) continue;
+                const int cc = G.cc[j];
+                const double r1 = G.r1[j], pp = G.pp[j], xj = L.xv[j];
+                if (cc) continue;
                 double atz = 0.0;
                 for (int k = P.colptr[j]; k < P.colptr[j + 1]; ++k)
                     atz += sp_a_csc(Y, k, s) * L.tv[P.rowidx[k]];
-                const double dx = (G.r1[j] - atz) / (G.pp[j] + reg);
-                const double x = L.xv[j] + dx;
+                const double dx = (r1 - atz) / (pp + reg);
+                const double x = xj + dx;
                 L.xv[j] = x;
                 mx[0] = fmax(mx[0], fabs(dx));
                 mx[1] = fmax(mx[1], fabs(x));
             }
             for (int i = SP_TID; i < m; i += SP_NT) {
-                if (!G.rc[i]) continue;
-                const double dz = L.tv[i];
-                const double zn = L.yv[i] + dz;
+                const int rc = G.rc[i];
+                const double dz = L.tv[i], yi = L.yv[i];
+                if (!rc) continue;
+                const double zn = yi + dz;
                 L.yv[i] = zn;
                 mx[0] = fmax(mx[0], fabs(dz));
                 mx[1] = fmax(mx[1], fabs(zn));
@@ -989,15 +992,16 @@ PHX_HD int sp_rounds(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds&
         double bad[1] = {0.0};
         for (int j = SP_TID; j < n; j += SP_NT) {
             const double x = L.xv[j], l = G.lb[j], u = G.ub[j], dc = P.dc[j];
+            const double qq = G.qq[j], pp = G.pp[j];
+            const int c = G.cc[j];
             if (x < l && (l - x) * dc > ptol * (1.0 + fabs(l * dc))) bad[0] = 1.0;
             if (x > u && (x - u) * dc > ptol * (1.0 + fabs(u * dc))) bad[0] = 1.0;
             double atz = 0.0;
             for (int k = P.colptr[j]; k < P.colptr[j + 1]; ++k)
                 atz += sp_a_csc(Y, k, s) * L.yv[P.rowidx[k]];
-            const double lam = (G.qq[j] + G.pp[j] * x + atz) / dc;
+            const double lam = (qq + pp * x + atz) / dc;
             G.r1[j] = lam;
             if (!(lam - lam == 0.0)) bad[0] = 1.0;   // non-finite x or y: no comparison would fail
-            const int c = G.cc[j];
             if (c == 0) {
                 if (fabs(lam) > dtol) bad[0] = 1.0;
             } else if (!(l == u)) {
@@ -1025,9 +1029,9 @@ PHX_HD int sp_rounds(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds&
         // ---- primal-dual active-set update ----
         for (int j = SP_TID; j < n; j += SP_NT) {
             const double l = G.lb[j], u = G.ub[j];
-            if (l == u) continue;
             const double x = L.xv[j], lam = G.r1[j], dc = P.dc[j];
             const int c = G.cc[j];
+            if (l == u) continue;
             if (c == 1 && lam < -dtol) G.cc[j] = 0;
             else if (c == 2 && lam > dtol) G.cc[j] = 0;
             else if (c == 0 && x < l && (l - x) * dc > ptol * (1.0 + fabs(l * dc))) { G.cc[j] = 1; L.xv[j] = l; }
@@ -1035,10 +1039,10 @@ PHX_HD int sp_rounds(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds&
         }
         for (int i = SP_TID; i < m; i += SP_NT) {
             const double bl = G.bl[i], bu = G.bu[i];
-            if (bl == bu) continue;
-            const double ax = G.ax[i], dr = P.dr[i];
-            const double y = -L.yv[i] * dr;
+            const double ax = G.ax[i], dr = P.dr[i], yi = L.yv[i];
             const int r = G.rc[i];
+            if (bl == bu) continue;
+            const double y = -yi * dr;
             if (r == 1 && y < -dtol) { G.rc[i] = 0; L.yv[i] = 0.0; }
             else if (r == 2 && y > dtol) { G.rc[i] = 0; L.yv[i] = 0.0; }
             else if (r == 0 && ax < bl && (bl - ax) / dr > ptol * (1.0 + fabs(bl / dr))) G.rc[i] = 1;

@@ -163,5 +163,9 @@ case "$1" in
        $J "test:tests/test_sslp.py tests/test_netdes.py tests/test_bench_settings.py tests/test_trajectories.py tests/test_gpu_parity.py" \
           "bench:r05_s38_c5a:--only C5a $A" "bench:r05_s38_c5b:--only C5b $A" "bench:r05_s38_c2:--only C2 $A" && \
        PHX_SP_PROF=1 $J "bench:r05_s38_c5a_spprof:--only C5a $A" ;;
+  s39) # ... the same for the KKT error, classification and active-set rounds: parity, C5a / C5b / C2, clocks
+       $J "test:tests/test_sslp.py tests/test_netdes.py tests/test_bench_settings.py tests/test_trajectories.py tests/test_gpu_parity.py" \
+          "bench:r05_s39_c5a:--only C5a $A" "bench:r05_s39_c5b:--only C5b $A" "bench:r05_s39_c2:--only C2 $A" && \
+       PHX_SP_PROF=1 $J "bench:r05_s39_c5b_spprof:--only C5b $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
