@@ -822,10 +822,14 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
             // division by the column's owner, once; the rows' products below
             // then need none)
             for (int j = WG_TID; j < n; j += WG_NT) {
-                if (L.cc[j]) { L.r1[j] = 0.0; continue; }
+                // (operands loaded before the branch: one round trip, the split
+                // layout's column vectors being global)
+                const int8_t cj = L.cc[j];
+                const double qq = L.qq[j], pp = L.pp[j], xj = L.xp[j];
+                if (cj) { L.r1[j] = 0.0; continue; }
                 double atz = 0.0;
                 for (int k = cp[j]; k < cp[j + 1]; ++k) atz += L.a[c2[k]] * L.z[ri[k]];
-                L.r1[j] = (-L.qq[j] - L.pp[j] * L.xp[j] - atz) / (L.pp[j] + reg);
+                L.r1[j] = (-qq - pp * xj - atz) / (pp + reg);
             }
             WG_SYNC();
             WG_TP(11);
@@ -894,14 +898,16 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
             const double* dz = BLK == 2 ? L.u : L.t;
             double dmax = 0.0, xmax = 0.0;
             for (int j = WG_TID; j < n; j += WG_NT) {
-                if (L.cc[j]) continue;
+                const int8_t cj = L.cc[j];
+                const double r1 = L.r1[j], pp = L.pp[j], xj = L.xp[j];
+                if (cj) continue;
                 double atz = 0.0;
                 for (int k = cp[j]; k < cp[j + 1]; ++k) {
                     const int q = L.pos[ri[k]];
                     if (q >= 0) atz += L.a[c2[k]] * dz[q];
                 }
-                const double dx = L.r1[j] - atz / (L.pp[j] + reg);
-                const double x = L.xp[j] + dx;
+                const double dx = r1 - atz / (pp + reg);
+                const double x = xj + dx;
                 L.xp[j] = x;
                 dmax = fmax(dmax, fabs(dx));
                 xmax = fmax(xmax, fabs(x));
@@ -928,15 +934,15 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
         for (int j = WG_TID; j < n; j += WG_NT) {
             const double x = L.xp[j];
             const double l = P.lb.at(j, s), u = P.ub.at(j, s);
-            const double dc = P.dc[j];
+            const double dc = P.dc[j], qq = L.qq[j], pp = L.pp[j];
+            const int8_t c = L.cc[j];
             if (x < l && (l - x) * dc > ptol * (1.0 + fabs(l * dc))) bad = true;
             if (x > u && (x - u) * dc > ptol * (1.0 + fabs(u * dc))) bad = true;
             double atz = 0.0;
             for (int k = cp[j]; k < cp[j + 1]; ++k) atz += L.a[c2[k]] * L.z[ri[k]];
-            const double lam = (L.qq[j] + L.pp[j] * x + atz) / dc;
+            const double lam = (qq + pp * x + atz) / dc;
             L.r1[j] = lam;
             if (!(lam - lam == 0.0)) bad = true;   // non-finite x or z: no comparison would fail
-            const int8_t c = L.cc[j];
             if (c == 0) {
                 if (fabs(lam) > dtol) bad = true;
             } else if (!(l == u)) {
@@ -1013,9 +1019,9 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
         int bi = -1;         // its element: column j, or n + row i
         for (int j = WG_TID; j < n; j += WG_NT) {
             const double l = P.lb.at(j, s), u = P.ub.at(j, s);
-            if (l == u) continue;
             const double x = L.xp[j], lam = L.r1[j], dc = P.dc[j];
             const int8_t c = L.cc[j];
+            if (l == u) continue;
             int8_t cn = c;
             double key = 0.0;
             if (c == 1 && lam < -dtol) { cn = 0; key = 1.0 + (-lam) / (1.0 - lam); }

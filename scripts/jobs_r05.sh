@@ -167,5 +167,8 @@ case "$1" in
        $J "test:tests/test_sslp.py tests/test_netdes.py tests/test_bench_settings.py tests/test_trajectories.py tests/test_gpu_parity.py" \
           "bench:r05_s39_c5a:--only C5a $A" "bench:r05_s39_c5b:--only C5b $A" "bench:r05_s39_c2:--only C2 $A" && \
        PHX_SP_PROF=1 $J "bench:r05_s39_c5b_spprof:--only C5b $A" ;;
+  s40) # workgroup solver: operands loaded before branching in the refinement / certificate / update loops -- parity, C2 / C5a
+       $J "test:tests/test_sslp.py tests/test_bench_settings.py tests/test_trajectories.py tests/test_gpu_parity.py" \
+          "bench:r05_s40_c2:--only C2 $A" "bench:r05_s40_c5a:--only C5a $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
