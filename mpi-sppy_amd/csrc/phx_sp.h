@@ -936,7 +936,10 @@ PHX_HD int sp_rounds(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds&
         if (!sp_factor(P, Y, G, L, s)) return 0;
         // ---- iterative refinement on the unregularised KKT (proximal point) ----
         for (int it = 0; it < O.refine_steps; ++it) {
-            for (int j = SP_TID; j < n; j += SP_NT) {
+            // the column residual from the data on the first step only: after
+            // a step it is reg dx exactly (phx_wg.h's refinement), written by
+            // the update below, so this phase and its barrier go
+            for (int j = SP_TID; j < (it == 0 ? n : 0); j += SP_NT) {
                 const int cc = G.cc[j];
                 const double qq = G.qq[j], pp = G.pp[j], xj = L.xv[j];
                 if (cc) { G.r1[j] = 0.0; L.hv[j] = 0.0; continue; }
@@ -947,7 +950,7 @@ PHX_HD int sp_rounds(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds&
                 G.r1[j] = r1;
                 L.hv[j] = r1 / (pp + reg);
             }
-            SP_SYNC();
+            if (it == 0) SP_SYNC();
             SP_TP(3);
             sp_rows(P, Y, s, L.xv, L.hv, [&](int i, double ax, double adr) {
                 const int rc = G.rc[i];
@@ -966,9 +969,14 @@ PHX_HD int sp_rounds(const Prob& P, const SpSym& Y, const SpScr& G, const SpLds&
                 double atz = 0.0;
                 for (int k = P.colptr[j]; k < P.colptr[j + 1]; ++k)
                     atz += sp_a_csc(Y, k, s) * L.tv[P.rowidx[k]];
-                const double dx = (r1 - atz) / (pp + reg);
+                const double ih = 1.0 / (pp + reg);
+                const double dx = (r1 - atz) * ih;
                 const double x = xj + dx;
                 L.xv[j] = x;
+                // -q - P x' - A'z' = r1 - P dx - A'dz = reg dx
+                const double rn = reg * dx;
+                G.r1[j] = rn;
+                L.hv[j] = rn * ih;
                 mx[0] = fmax(mx[0], fabs(dx));
                 mx[1] = fmax(mx[1], fabs(x));
             }

@@ -820,8 +820,11 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
         for (int it = 0; it < O.refine_steps; ++it) {
             // r1 = H^-1 (-q - P x - A'z) on the free columns, 0 elsewhere (the
             // division by the column's owner, once; the rows' products below
-            // then need none)
-            for (int j = WG_TID; j < n; j += WG_NT) {
+            // then need none).  Only the first step forms it from the data:
+            // after a step the column residual is reg dx exactly (the
+            // regularised system's definition, see the update below), so the
+            // update writes the next step's r1 and this phase's barrier goes
+            for (int j = WG_TID; j < (it == 0 ? n : 0); j += WG_NT) {
                 // (operands loaded before the branch: one round trip, the split
                 // layout's column vectors being global)
                 const int8_t cj = L.cc[j];
@@ -831,7 +834,7 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
                 for (int k = cp[j]; k < cp[j + 1]; ++k) atz += L.a[c2[k]] * L.z[ri[k]];
                 L.r1[j] = (-qq - pp * xj - atz) / (pp + reg);
             }
-            WG_SYNC();
+            if (it == 0) WG_SYNC();
             WG_TP(11);
             // t = A_R (x + H^-1 r) - b_R: a quad per active row
             for (int q = WG_QID; q < ma; q += WG_QN) {
@@ -906,9 +909,14 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
                     const int q = L.pos[ri[k]];
                     if (q >= 0) atz += L.a[c2[k]] * dz[q];
                 }
-                const double dx = r1 - atz / (pp + reg);
+                // (P + reg) dx = (P + reg) r1 - A'dz, so the unregularised
+                // residual after the step, -q - P x' - A'z', is
+                // (P + reg) r1 - P dx - A'dz = reg dx: the next step's r1
+                const double ih = 1.0 / (pp + reg);
+                const double dx = r1 - atz * ih;
                 const double x = xj + dx;
                 L.xp[j] = x;
+                L.r1[j] = reg * dx * ih;
                 dmax = fmax(dmax, fabs(dx));
                 xmax = fmax(xmax, fabs(x));
             }

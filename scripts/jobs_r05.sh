@@ -170,5 +170,9 @@ case "$1" in
   s40) # workgroup solver: operands loaded before branching in the refinement / certificate / update loops -- parity, C2 / C5a
        $J "test:tests/test_sslp.py tests/test_bench_settings.py tests/test_trajectories.py tests/test_gpu_parity.py" \
           "bench:r05_s40_c2:--only C2 $A" "bench:r05_s40_c5a:--only C5a $A" ;;
+  s41) # refinement: the column residual after a step is reg dx (no recomputation, one barrier less per step) -- parity, C2 / C5a / C5b, clocks
+       $J "test:tests/test_sslp.py tests/test_netdes.py tests/test_bench_settings.py tests/test_trajectories.py tests/test_gpu_parity.py" \
+          "bench:r05_s41_c2:--only C2 $A" "bench:r05_s41_c5a:--only C5a $A" "bench:r05_s41_c5b:--only C5b $A" && \
+       PHX_WG_PROF=1 $J "bench:r05_s41_c2_wgprof:--only C2 $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
