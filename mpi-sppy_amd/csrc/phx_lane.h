@@ -1027,14 +1027,30 @@ PHX_LD void kkt_refine(const Data<PT>& D, const AMul<PT>& am, const KFactor<PT>&
     // mat-vec -- kept 12 more values live across the loop: 12 -> 72 B of
     // scratch per lane in the warm kernel, r04.)
     double x2 = 0.0;
+#ifdef PHX_REFINE_CARRY
+    // (opt-in) the column residual from the data once: after a step it is
+    // reg d exactly -- (P + reg) d = g - A'dz, so -q - P x' - A'z' = g - P d
+    // - A'dz = reg d on the free columns (the others are multiplied by hf = 0)
+    // -- carried to the next step instead of a transposed mat-vec per step
+    double g[NN];
+    {
+        double atz[NN];
+        D.matvec_t(z, atz);
+        PHX_UNROLL for (int j = 0; j < PT::n(); ++j)
+            g[j] = (PT::col_slot(j) >= 0 ? -R.q(j) - D.p(j) * xp[j] : -R.q(j)) - atz[j];
+    }
+#endif
     PHX_REFINE_LOOP for (int it = 0; it < KKT_REFINE; ++it) {
-        double g[NN], t[MM];
+#ifndef PHX_REFINE_CARRY
+        double g[NN];
         {
             double atz[NN];
             D.matvec_t(z, atz);
             PHX_UNROLL for (int j = 0; j < PT::n(); ++j)
                 g[j] = (PT::col_slot(j) >= 0 ? -R.q(j) - D.p(j) * xp[j] : -R.q(j)) - atz[j];
         }
+#endif
+        double t[MM];
         {
             // t = A_R (xp + H_F g) - b_R: one mat-vec of the sum (the same
             // rounding as the two products it replaces, to eps |A| |x|)
@@ -1051,6 +1067,9 @@ PHX_LD void kkt_refine(const Data<PT>& D, const AMul<PT>& am, const KFactor<PT>&
             const double d = (g[j] - atdz[j]) * hf[j];
             xp[j] += d;
             d2 += d * d;
+#ifdef PHX_REFINE_CARRY
+            g[j] = KKT_REG * d;
+#endif
         }
         PHX_UNROLL for (int i = 0; i < PT::m(); ++i) {
             z[i] += t[i];

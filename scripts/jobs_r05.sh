@@ -174,5 +174,12 @@ case "$1" in
        $J "test:tests/test_sslp.py tests/test_netdes.py tests/test_bench_settings.py tests/test_trajectories.py tests/test_gpu_parity.py" \
           "bench:r05_s41_c2:--only C2 $A" "bench:r05_s41_c5a:--only C5a $A" "bench:r05_s41_c5b:--only C5b $A" && \
        PHX_WG_PROF=1 $J "bench:r05_s41_c2_wgprof:--only C2 $A" ;;
+  s42) # lane refinement: the column residual carried as reg d (PHX_REFINE_CARRY) -- the GPU suite under it, then A/B on one box
+       PHX_LANE_DEFS=PHX_REFINE_CARRY $J "test:tests" && \
+       $J "bench:r05_s42_bench:$H" && PHX_LANE_DEFS=PHX_REFINE_CARRY $J "bench:r05_s42_bench_carry:$H" && \
+       $J "bench:r05_s42_1m:$M" && PHX_LANE_DEFS=PHX_REFINE_CARRY $J "bench:r05_s42_1m_carry:$M" && \
+       $J "bench:r05_s42_c3s8:$S8" && PHX_LANE_DEFS=PHX_REFINE_CARRY $J "bench:r05_s42_c3s8_carry:$S8" && \
+       $J "bench:r05_s42_c4:--only C4 $A" && PHX_LANE_DEFS=PHX_REFINE_CARRY $J "bench:r05_s42_c4_carry:--only C4 $A" && \
+       $J "bench:r05_s42_bench2:$H" && PHX_LANE_DEFS=PHX_REFINE_CARRY $J "bench:r05_s42_bench_carry2:$H" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
