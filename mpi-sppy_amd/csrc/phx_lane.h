@@ -70,6 +70,19 @@ typedef unsigned long long uint64_t;
 #else
 #define PHX_REFINE_LOOP PHX_NOUNROLL
 #endif
+// The refinement carries its column residual from step to step (kkt_refine's
+// CARRY) in every kernel but the two-wave fused build; PHX_REFINE_RECOMPUTE
+// recomputes it everywhere, PHX_FZR2_CARRY carries it there too.
+#ifdef PHX_REFINE_RECOMPUTE
+#define PHX_CARRY_DEF false
+#else
+#define PHX_CARRY_DEF true
+#endif
+#ifdef PHX_FZR2_CARRY
+#define PHX_FZR2_CARRY_DEF PHX_CARRY_DEF
+#else
+#define PHX_FZR2_CARRY_DEF false
+#endif
 
 // Diagnostics hook (the CPU emulation defines it to record why a lane failed;
 // a no-op in the GPU kernels).
@@ -1005,7 +1018,17 @@ PHX_LD bool kkt_factor(const Data<PT>& D, const AMul<PT>& am, KFactor<PT>& K) {
 // value of a non-free column, R.b(i) the active side of row i (a
 // proximal-point iteration: it converges to the solution nearest the start on
 // degenerate faces).
+// The column residual g = -q - P x - A'z (P: the prox weights of the nonant
+// columns) of the right-hand side R at (xp, z).
 template <class PT, class RHS>
+PHX_LD void col_residual(const Data<PT>& D, const RHS& R, const double* xp, const double* z, double* g) {
+    double atz[PT::NMAX_N];
+    D.matvec_t(z, atz);
+    PHX_UNROLL for (int j = 0; j < PT::n(); ++j)
+        g[j] = (PT::col_slot(j) >= 0 ? -R.q(j) - D.p(j) * xp[j] : -R.q(j)) - atz[j];
+}
+
+template <class PT, class RHS, bool CARRY = PHX_CARRY_DEF>
 PHX_LD void kkt_refine(const Data<PT>& D, const AMul<PT>& am, const KFactor<PT>& K, const RHS& R, double* xp,
                        double* z) {
     constexpr int NN = PT::NMAX_N, MM = PT::NMAX_M;
@@ -1023,33 +1046,18 @@ PHX_LD void kkt_refine(const Data<PT>& D, const AMul<PT>& am, const KFactor<PT>&
 #endif
     // x2, the stop's scale, is the first step's (the step that moves the
     // point; the later ones change it by the refinement's corrections only).
-    // (Carrying A'z from step to step -- A'z += A't, 12 adds instead of a
-    // mat-vec -- kept 12 more values live across the loop: 12 -> 72 B of
-    // scratch per lane in the warm kernel, r04.)
     double x2 = 0.0;
-#ifdef PHX_REFINE_CARRY
-    // (opt-in) the column residual from the data once: after a step it is
-    // reg d exactly -- (P + reg) d = g - A'dz, so -q - P x' - A'z' = g - P d
-    // - A'dz = reg d on the free columns (the others are multiplied by hf = 0)
-    // -- carried to the next step instead of a transposed mat-vec per step
+    // CARRY: the column residual from the data once; after a step it is reg d
+    // exactly -- (P + reg) d = g - A'dz on the free columns, so -q - P x' - A'z'
+    // = g - P d - A'dz = reg d (the others are multiplied by hf = 0) -- and is
+    // carried to the next step instead of a transposed mat-vec per step.
+    // (Carrying A'z instead kept 12 more values live across the loop, 12 -> 72 B
+    // of scratch in the warm kernel, r04; g replaces the step's own g.  The
+    // two-wave fused build recomputes it: carried, it spilled more, r05 s42.)
     double g[NN];
-    {
-        double atz[NN];
-        D.matvec_t(z, atz);
-        PHX_UNROLL for (int j = 0; j < PT::n(); ++j)
-            g[j] = (PT::col_slot(j) >= 0 ? -R.q(j) - D.p(j) * xp[j] : -R.q(j)) - atz[j];
-    }
-#endif
+    if (CARRY) col_residual<PT>(D, R, xp, z, g);
     PHX_REFINE_LOOP for (int it = 0; it < KKT_REFINE; ++it) {
-#ifndef PHX_REFINE_CARRY
-        double g[NN];
-        {
-            double atz[NN];
-            D.matvec_t(z, atz);
-            PHX_UNROLL for (int j = 0; j < PT::n(); ++j)
-                g[j] = (PT::col_slot(j) >= 0 ? -R.q(j) - D.p(j) * xp[j] : -R.q(j)) - atz[j];
-        }
-#endif
+        if (!CARRY) col_residual<PT>(D, R, xp, z, g);
         double t[MM];
         {
             // t = A_R (xp + H_F g) - b_R: one mat-vec of the sum (the same
@@ -1067,9 +1075,7 @@ PHX_LD void kkt_refine(const Data<PT>& D, const AMul<PT>& am, const KFactor<PT>&
             const double d = (g[j] - atdz[j]) * hf[j];
             xp[j] += d;
             d2 += d * d;
-#ifdef PHX_REFINE_CARRY
-            g[j] = KKT_REG * d;
-#endif
+            if (CARRY) g[j] = KKT_REG * d;
         }
         PHX_UNROLL for (int i = 0; i < PT::m(); ++i) {
             z[i] += t[i];
@@ -1154,7 +1160,7 @@ struct RhsSlot {      // d/dqn[t]: unit linear term on slot t's column, homogene
 // by its quasi-definite regularisation (P+reg, -reg) and iterative refinement
 // from the given (xp, z).  Non-free columns are set to their bound.  false if
 // the Schur complement is not positive definite.
-template <class PT>
+template <class PT, bool CARRY = PHX_CARRY_DEF>
 PHX_LD bool kkt_solve(const Data<PT>& D, const ASet<PT>& a, double* xp, double* z) {
     KFactor<PT> K;
     const AMul<PT> am(a);
@@ -1175,7 +1181,7 @@ PHX_LD bool kkt_solve(const Data<PT>& D, const ASet<PT>& a, double* xp, double* 
         PHX_UNROLL for (int i = 0; i < PT::m(); ++i) { opaque(z[i]); z[i] = z0[i]; }
     }
 #endif
-    kkt_refine<PT>(D, am, K, RhsFull<PT>{D, a}, xp, z);
+    kkt_refine<PT, RhsFull<PT>, CARRY>(D, am, K, RhsFull<PT>{D, a}, xp, z);
     return true;
 }
 
@@ -1416,10 +1422,10 @@ PHX_LD void write_certified(const LaneIO& io, const Data<PT>& D, int sc, const A
 // One round with the given data: KKT solve, certificate, active-set update
 // (0 certified, 1 active set changed, 2 not certified and nothing to change,
 // 3 the Schur complement was not positive definite).
-template <class PT>
+template <class PT, bool CARRY = PHX_CARRY_DEF>
 PHX_LD int as_round(const LaneIO& io, const Data<PT>& D, ASet<PT>& a, double* xp, double* z, int r) {
     PHX_LANE_STAT(0);
-    if (!kkt_solve<PT>(D, a, xp, z)) return 3;
+    if (!kkt_solve<PT, CARRY>(D, a, xp, z)) return 3;
     return certify_update<PT>(D, a, xp, z, io.kkt_tol, r >= io.single_after);
 }
 // r0: the index of the first round (the fused kernel runs round 0 itself)
@@ -2126,7 +2132,7 @@ __device__ __forceinline__ void compact_lane(bool still, int sc, int32_t* out, i
 // REG (the one-wave-per-SIMD build, 512 registers): every round runs on the
 // data in registers -- the other builds re-load it per round (kept live across
 // the round loop it spilled; a re-load is a memory round trip per round)
-template <class PT, bool REG = false>
+template <class PT, bool REG = false, bool CARRY = PHX_CARRY_DEF>
 __device__ __forceinline__ void warm_fused(const LaneIO& io) {
     const FusedW& f = io.fz;
     constexpr int NS = PT::nslot() > 0 ? PT::nslot() : 1;
@@ -2184,9 +2190,9 @@ __device__ __forceinline__ void warm_fused(const LaneIO& io) {
         int c;
         if (REG) {
             const Data<PT> D0(io, sc, av, wv, rv, xb);
-            c = io.warm_rounds > 0 ? as_round<PT>(io, D0, a, xp, z, 0) : 2;
+            c = io.warm_rounds > 0 ? as_round<PT, CARRY>(io, D0, a, xp, z, 0) : 2;
             int nr = 1;
-            PHX_NOUNROLL for (int r = 1; r < io.warm_rounds && c == 1; ++r, ++nr) c = as_round<PT>(io, D0, a, xp, z, r);
+            PHX_NOUNROLL for (int r = 1; r < io.warm_rounds && c == 1; ++r, ++nr) c = as_round<PT, CARRY>(io, D0, a, xp, z, r);
             // (diagnostics: the wavefront's most rounds, PHX_LANE_STAMPS=1)
             if (io.stamps) {
                 int wmax = 0;

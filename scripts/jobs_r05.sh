@@ -181,5 +181,11 @@ case "$1" in
        $J "bench:r05_s42_c3s8:$S8" && PHX_LANE_DEFS=PHX_REFINE_CARRY $J "bench:r05_s42_c3s8_carry:$S8" && \
        $J "bench:r05_s42_c4:--only C4 $A" && PHX_LANE_DEFS=PHX_REFINE_CARRY $J "bench:r05_s42_c4_carry:--only C4 $A" && \
        $J "bench:r05_s42_bench2:$H" && PHX_LANE_DEFS=PHX_REFINE_CARRY $J "bench:r05_s42_bench_carry2:$H" ;;
+  s43) # carried refinement residual by default except in the two-wave fused build -- the GPU suite, then A/B against PHX_REFINE_RECOMPUTE
+       $J "test:tests" && \
+       $J "bench:r05_s43_bench:$H" && PHX_LANE_DEFS=PHX_REFINE_RECOMPUTE $J "bench:r05_s43_bench_rc:$H" && \
+       $J "bench:r05_s43_bench2:$H" && PHX_LANE_DEFS=PHX_REFINE_RECOMPUTE $J "bench:r05_s43_bench_rc2:$H" && \
+       $J "bench:r05_s43_1m:$M" && PHX_LANE_DEFS=PHX_REFINE_RECOMPUTE $J "bench:r05_s43_1m_rc:$M" && \
+       $J "bench:r05_s43_c3s8:$S8" "bench:r05_s43_c4:--only C4 $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
