@@ -26,6 +26,44 @@
 
 namespace phx {
 
+#if defined(__HIP_DEVICE_COMPILE__)
+// Cross-lane reductions of one wavefront by DPP moves (VALU, a few cycles each)
+// instead of __shfl_xor's ds_bpermute (an LDS round trip per step and 32-bit
+// half).  OP 0: sum, 1: max, 2: min.  The butterfly's pairing is kept (quad_perm
+// [1,0,3,2] = xor 1, [2,3,0,1] = xor 2; on values equal within each quad,
+// row_half_mirror = xor 4 and row_mirror = xor 8), so the results are the
+// same bits as the __shfl_xor butterflies they replace.
+template <int OP, int CTRL, int ROWMASK>
+__device__ __forceinline__ double dpp_op(double v) {
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u & 0xffffffffull), CTRL, ROWMASK, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, ROWMASK, 0xf, false);
+    const double w = __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+    return OP == 0 ? v + w : (OP == 1 ? fmax(v, w) : fmin(v, w));
+}
+// over a quad (four adjacent lanes; all four end with it)
+template <int OP>
+__device__ __forceinline__ double quad_reduce(double v) {
+    v = dpp_op<OP, 0xB1, 0xf>(v);
+    return dpp_op<OP, 0x4E, 0xf>(v);
+}
+// over the wavefront (every lane active): rows by mirrors, then the row
+// broadcasts of lanes 15 and 31 leave the total in lane 63, read back
+// uniformly (readlane is 32-bit: both halves)
+template <int OP>
+__device__ __forceinline__ double wave_reduce(double v) {
+    v = quad_reduce<OP>(v);
+    v = dpp_op<OP, 0x141, 0xf>(v);    // row_half_mirror
+    v = dpp_op<OP, 0x140, 0xf>(v);    // row_mirror
+    v = dpp_op<OP, 0x142, 0xa>(v);    // row_bcast:15 into rows 1, 3
+    v = dpp_op<OP, 0x143, 0xc>(v);    // row_bcast:31 into rows 2, 3
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u & 0xffffffffull), 63);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), 63);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+#endif
+
 // INFEASIBLE: a Farkas certificate proves the subproblem's feasible set empty
 // (the reference's infeasible termination, spopt.py:175-194: scenario_feasible
 // = False); ITER_LIMIT / NUMERIC_FAIL are solve failures, not infeasibility.

@@ -74,8 +74,7 @@ namespace phx {
 #endif
 PHX_HD double sp_quad_sum(double v) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    v += __shfl_xor(v, 1, 64);
-    v += __shfl_xor(v, 2, 64);
+    v = quad_reduce<0>(v);
 #endif
     return v;
 }
@@ -286,7 +285,7 @@ template <int K>
 PHX_HD void sp_reduce(double* v, double* red, int op) {
 #if defined(__HIP_DEVICE_COMPILE__)
     for (int q = 0; q < K; ++q)
-        for (int o = 32; o > 0; o >>= 1) v[q] = sp_op(v[q], __shfl_xor(v[q], o, 64), op);
+        v[q] = op == 0 ? wave_reduce<0>(v[q]) : (op == 1 ? wave_reduce<1>(v[q]) : wave_reduce<2>(v[q]));
     const int nw = (int)(blockDim.x >> 6), w = (int)(threadIdx.x >> 6);
     __syncthreads();
     if ((threadIdx.x & 63) == 0)

@@ -166,7 +166,7 @@ PHX_HD WgLds wg_carve(void* base, int n, int m, int nnz, void* gbase = nullptr, 
 // wavefront results through LDS (two barriers: red may be reused right after)
 PHX_HD double wg_max(double v, double* red) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+    v = wave_reduce<1>(v);
     __syncthreads();
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
     __syncthreads();
@@ -181,10 +181,8 @@ PHX_HD double wg_max(double v, double* red) {
 // max of two values over the workgroup in one LDS round (two barriers)
 PHX_HD void wg_max2(double& a, double& b, double* red) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    for (int o = 32; o > 0; o >>= 1) {
-        a = fmax(a, __shfl_xor(a, o, 64));
-        b = fmax(b, __shfl_xor(b, o, 64));
-    }
+    a = wave_reduce<1>(a);
+    b = wave_reduce<1>(b);
     __syncthreads();
     if ((threadIdx.x & 63) == 0) {
         red[threadIdx.x >> 6] = a;
@@ -232,8 +230,7 @@ PHX_HD void wg_argmax(double& key, int& el, double* red) {
 // sum of a value over a quad (its four threads end with the same sum)
 PHX_HD double wg_quad_sum(double v) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    v += __shfl_xor(v, 1, 64);
-    v += __shfl_xor(v, 2, 64);
+    v = quad_reduce<0>(v);
 #endif
     return v;
 }
@@ -1103,7 +1100,7 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
 // LDS), identity on the host
 PHX_HD double wg_sum(double v, double* red) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    v = wave_reduce<0>(v);
     __syncthreads();
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
     __syncthreads();

@@ -187,5 +187,9 @@ case "$1" in
        $J "bench:r05_s43_bench2:$H" && PHX_LANE_DEFS=PHX_REFINE_RECOMPUTE $J "bench:r05_s43_bench_rc2:$H" && \
        $J "bench:r05_s43_1m:$M" && PHX_LANE_DEFS=PHX_REFINE_RECOMPUTE $J "bench:r05_s43_1m_rc:$M" && \
        $J "bench:r05_s43_c3s8:$S8" "bench:r05_s43_c4:--only C4 $A" ;;
+  s44) # workgroup / sparse cross-lane sums and maxes by DPP instead of ds_bpermute shuffles -- parity, C2 / C5a / C5b, clocks
+       $J "test:tests/test_sslp.py tests/test_netdes.py tests/test_bench_settings.py tests/test_trajectories.py tests/test_gpu_parity.py tests/test_wg_blk.py" \
+          "bench:r05_s44_c2:--only C2 $A" "bench:r05_s44_c5a:--only C5a $A" "bench:r05_s44_c5b:--only C5b $A" && \
+       PHX_WG_PROF=1 $J "bench:r05_s44_c2_wgprof:--only C2 $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
