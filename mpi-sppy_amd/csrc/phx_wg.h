@@ -729,20 +729,32 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
                 const double d1 = L.Sm[b * ld + b] - (e * id0) * e;
                 if (!(d1 > 0.0)) { spd = false; break; }
                 const double sd0 = sqrt(d0), sd1 = sqrt(d1), id1 = 1.0 / d1;
-                for (int i = b + 1 + WG_QID; i < ma; i += WG_QN) {
+                // (a group of gw threads per trailing row, as wide as the rows
+                // left allow: gw = 16 at 16 rows or fewer, 8 at 32, 4 at 64 --
+                // the step's time is its longest row's entries over gw; every
+                // entry is still updated by one thread with the same
+                // expression, so the factor does not depend on gw)
+#if defined(__HIP_DEVICE_COMPILE__)
+                const int nrow = ma - b - 1;
+                const int gs = nrow <= WG_NT / 16 ? 4 : (nrow <= WG_NT / 8 ? 3 : (nrow <= WG_NT / 4 ? 2 : 1));
+                const int gw = 1 << gs, gid = WG_TID >> gs, gl = WG_TID & (gw - 1), gn = WG_NT >> gs;
+#else
+                const int gw = 1, gid = 0, gl = 0, gn = 1;
+#endif
+                for (int i = b + 1 + gid; i < ma; i += gn) {
                     double* row = L.Sm + (size_t)i * ld;
                     const double lia = row[a];
                     const double f0 = lia * id0;
                     const double lib = row[b] - f0 * e;
                     const double f1 = lib * id1;
-                    int k = b + 1 + WG_QL;
-                    for (; k <= i; k += WG_QW) {
+                    int k = b + 1 + gl;
+                    for (; k <= i; k += gw) {
                         const double ga = L.Sm[k * ld + a];
                         const double h = L.Sm[k * ld + b] - (ga * id0) * e;
                         const double t = row[k] - f0 * ga;
                         row[k] = t - f1 * h;
                     }
-                    if (WG_QL == 0) {
+                    if (gl == 0) {
                         L.Sm[a * ld + i] = lia / sd0;
                         L.Sm[b * ld + i] = lib / sd1;
                     }

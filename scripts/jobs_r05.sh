@@ -191,5 +191,9 @@ case "$1" in
        $J "test:tests/test_sslp.py tests/test_netdes.py tests/test_bench_settings.py tests/test_trajectories.py tests/test_gpu_parity.py tests/test_wg_blk.py" \
           "bench:r05_s44_c2:--only C2 $A" "bench:r05_s44_c5a:--only C5a $A" "bench:r05_s44_c5b:--only C5b $A" && \
        PHX_WG_PROF=1 $J "bench:r05_s44_c2_wgprof:--only C2 $A" ;;
+  s45) # workgroup Cholesky: thread groups per trailing row as wide as the rows left allow -- parity, C2 / C5a, clocks
+       $J "test:tests/test_sslp.py tests/test_bench_settings.py tests/test_trajectories.py tests/test_gpu_parity.py tests/test_wg_blk.py" \
+          "bench:r05_s45_c2:--only C2 $A" "bench:r05_s45_c5a:--only C5a $A" && \
+       PHX_WG_PROF=1 $J "bench:r05_s45_c2_wgprof:--only C2 $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
