@@ -195,5 +195,10 @@ case "$1" in
        $J "test:tests/test_sslp.py tests/test_bench_settings.py tests/test_trajectories.py tests/test_gpu_parity.py tests/test_wg_blk.py" \
           "bench:r05_s45_c2:--only C2 $A" "bench:r05_s45_c5a:--only C5a $A" && \
        PHX_WG_PROF=1 $J "bench:r05_s45_c2_wgprof:--only C2 $A" ;;
+  s46) # the sparse interior point's stopping tolerance (ipm_tol; the classification follows it): C5b / C5a Iter0 and step
+       $J "bench:r05_s46_c5b:--only C5b $A" "bench:r05_s46_c5b_t8:--only C5b $A --so {\"ipm_tol\":1e-8}" \
+          "bench:r05_s46_c5b_t6:--only C5b $A --so {\"ipm_tol\":1e-6}" \
+          "bench:r05_s46_c5a:--only C5a $A" "bench:r05_s46_c5a_t8:--only C5a $A --so {\"ipm_tol\":1e-8}" \
+          "bench:r05_s46_c5a_t6:--only C5a $A --so {\"ipm_tol\":1e-6}" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
