@@ -323,7 +323,10 @@ inline std::string lane_kernel_source(const LaneStructure& L, int warm_waves = 1
          "}\n";
     // phx_iterk fused mode, after the last enqueued iteration: the decision on
     // its conv (the next warm launch's prologue does it otherwise)
-    o << "extern \"C\" __global__ void __launch_bounds__(64) phx_fz_tail(phx_lane::LaneIO io) {\n"
+    // (and the copies the host reads after the drain, whether or not the loop
+    // stopped earlier: as the copy dispatches they replace)
+    o << "extern \"C\" __global__ void __launch_bounds__(64) phx_fz_tail(phx_lane::LaneIO io, phx_lane::TailCopy tc) {\n"
+         "  phx_lane::tail_copy(tc);\n"
          "  if (phx_lane::gated(io.gate)) return;\n"
          "  (void)phx_lane::fz_decide(io.fz, io.fz.iter);\n"
          "}\n";

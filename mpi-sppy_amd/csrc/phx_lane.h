@@ -225,6 +225,20 @@ struct LaneIO {
     uint64_t* stamps;      // diagnostics (PHX_LANE_STAMPS=1): [block][8] wall-clock phase stamps, or null
 };
 
+// phx_iterk fused mode, the last iteration: the small results the host reads
+// after the drain, stored by the tail kernel (phx_fz_tail) instead of three
+// copy dispatches behind it (~5 us each on the loop's stream).  Each pointer
+// pair is skipped when its destination is null.
+struct TailCopy {
+    int32_t* left_dst;          // the last solve's leftover count (mapped host memory)
+    const int32_t* left_src;
+    double* seg_dst;            // the last test's convergence sums (device)
+    const double* seg_src;
+    int32_t nseg;
+    double* exp_dst;            // Iter0's expectations (mapped host memory)
+    const double* exp_src;
+};
+
 // Phase stamps of phx_lane_warm (lane 0 of each wavefront; 100 MHz wall clock):
 // 0 entry, 1 after the prologue, 2 after Update_W, 3 after the solve,
 // 4 after the compaction, 5 after the epilogue.
@@ -1862,6 +1876,15 @@ __device__ __forceinline__ double wave_sum(double v) {
     const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u & 0xffffffffull), 63);
     const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), 63);
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// (one wavefront; vector stores)
+__device__ __forceinline__ void tail_copy(const TailCopy& tc) {
+    const int t = (int)threadIdx.x;
+    if (tc.left_dst && t == 0) tc.left_dst[0] = *(const volatile int32_t*)tc.left_src;
+    if (tc.seg_dst)
+        for (int g = t; g < tc.nseg; g += (int)blockDim.x) tc.seg_dst[g] = tc.seg_src[g];
+    if (tc.exp_dst && t < 3) tc.exp_dst[t] = tc.exp_src[t];
 }
 
 __device__ __forceinline__ void publish_progress(IterkProgress* p, int iter, int done, double conv) {

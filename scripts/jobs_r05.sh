@@ -200,5 +200,8 @@ case "$1" in
           "bench:r05_s46_c5b_t6:--only C5b $A --so {\"ipm_tol\":1e-6}" \
           "bench:r05_s46_c5a:--only C5a $A" "bench:r05_s46_c5a_t8:--only C5a $A --so {\"ipm_tol\":1e-8}" \
           "bench:r05_s46_c5a_t6:--only C5a $A --so {\"ipm_tol\":1e-6}" ;;
+  s47) # Iter0 bookkeeping with batched loads and a parallel fold; the fused loop's last copies stored by its tail kernel
+       $J "test:tests" && $J "bench:r05_s47_bench:$H" "bench:r05_s47_bench2:$H" "bench:r05_s47_1m:$M" "bench:r05_s47_c3s8:$S8" \
+          "prof:r05_s47_prof:$H --ar-probe 0" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
