@@ -227,33 +227,6 @@ PHX_HD void wg_argmax(double& key, int& el, double* red) {
 #endif
 }
 
-// Thread groups of 2^gs adjacent threads for a phase over `rows` items, as
-// wide as the item count allows (gs 4: sixteen threads, one DPP row, at 16
-// items or fewer; 3: eight at 32; 2: a quad above), and the sum over a group
-// (every thread of the group ends with it).  Host: one thread.
-struct WgGroup {
-    int gs, gw, gid, gl, gn;   // log2 width, width, group id, thread in group, groups
-};
-PHX_HD WgGroup wg_group(int rows) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    const int gs = rows <= WG_NT / 16 ? 4 : (rows <= WG_NT / 8 ? 3 : 2);
-    return WgGroup{gs, 1 << gs, WG_TID >> gs, WG_TID & ((1 << gs) - 1), WG_NT >> gs};
-#else
-    (void)rows;
-    return WgGroup{0, 1, 0, 0, 1};
-#endif
-}
-PHX_HD double wg_group_sum(double v, int gs) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    v = quad_reduce<0>(v);
-    if (gs >= 3) v = dpp_op<0, 0x141, 0xf>(v);    // row_half_mirror: the two quads of an eight
-    if (gs >= 4) v = dpp_op<0, 0x140, 0xf>(v);    // row_mirror: the two eights of a row
-#else
-    (void)gs;
-#endif
-    return v;
-}
-
 // sum of a value over a quad (its four threads end with the same sum)
 PHX_HD double wg_quad_sum(double v) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -872,20 +845,18 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
             }
             if (it == 0) WG_SYNC();
             WG_TP(11);
-            // t = A_R (x + H^-1 r) - b_R: a thread group per active row (as
-            // wide as the active rows allow: wg_group)
-            const WgGroup gr = wg_group(ma);
-            for (int q = gr.gid; q < ma; q += gr.gn) {
+            // t = A_R (x + H^-1 r) - b_R: a quad per active row
+            for (int q = WG_QID; q < ma; q += WG_QN) {
                 const int i = L.ar[q];
                 double adr = 0.0, ax = 0.0;
-                for (int k = rp[i] + gr.gl; k < rp[i + 1]; k += gr.gw) {
+                for (int k = rp[i] + WG_QL; k < rp[i + 1]; k += WG_QW) {
                     const int j = ci[k];
                     ax += L.a[k] * L.xp[j];
                     adr += L.a[k] * L.r1[j];
                 }
-                ax = wg_group_sum(ax, gr.gs);
-                adr = wg_group_sum(adr, gr.gs);
-                if (gr.gl == 0) {
+                ax = wg_quad_sum(ax);
+                adr = wg_quad_sum(adr);
+                if (WG_QL == 0) {
                     const double b = L.rc[i] == 1 ? P.bl.at(i, s) : P.bu.at(i, s);
                     L.t[q] = adr - (b - ax);
                 }
@@ -908,31 +879,30 @@ PHX_HD int wg_warm(const Prob& P, const State& St, const WgPairs& G, const Opts&
                 }
                 WG_SYNC();
             } else {
-            // u = L^-1 t ; then t = L^-T u (dz, compact order); a thread group
-            // per row / column (gr: as wide as the ma rows allow)
-            for (int i = gr.gid; i < ma; i += gr.gn) {
+            // u = L^-1 t ; then t = L^-T u (dz, compact order)
+            for (int i = WG_QID; i < ma; i += WG_QN) {
                 double v0 = 0.0, v1 = 0.0;
                 const double* row = L.Sm + (size_t)i * ld;
-                int k = gr.gl;
-                for (; k + gr.gw <= i; k += 2 * gr.gw) {
+                int k = WG_QL;
+                for (; k + WG_QW <= i; k += 2 * WG_QW) {
                     v0 += row[k] * L.t[k];
-                    v1 += row[k + gr.gw] * L.t[k + gr.gw];
+                    v1 += row[k + WG_QW] * L.t[k + WG_QW];
                 }
-                for (; k <= i; k += gr.gw) v0 += row[k] * L.t[k];
-                const double v = wg_group_sum(v0 + v1, gr.gs);
-                if (gr.gl == 0) L.u[i] = v;
+                for (; k <= i; k += WG_QW) v0 += row[k] * L.t[k];
+                const double v = wg_quad_sum(v0 + v1);
+                if (WG_QL == 0) L.u[i] = v;
             }
             WG_SYNC();
-            for (int k = gr.gid; k < ma; k += gr.gn) {
+            for (int k = WG_QID; k < ma; k += WG_QN) {
                 double v0 = 0.0, v1 = 0.0;
-                int i = k + gr.gl;
-                for (; i + gr.gw < ma; i += 2 * gr.gw) {
+                int i = k + WG_QL;
+                for (; i + WG_QW < ma; i += 2 * WG_QW) {
                     v0 += L.Sm[i * ld + k] * L.u[i];
-                    v1 += L.Sm[(i + gr.gw) * ld + k] * L.u[i + gr.gw];
+                    v1 += L.Sm[(i + WG_QW) * ld + k] * L.u[i + WG_QW];
                 }
-                for (; i < ma; i += gr.gw) v0 += L.Sm[i * ld + k] * L.u[i];
-                const double v = wg_group_sum(v0 + v1, gr.gs);
-                if (gr.gl == 0) L.t[k] = v;
+                for (; i < ma; i += WG_QW) v0 += L.Sm[i * ld + k] * L.u[i];
+                const double v = wg_quad_sum(v0 + v1);
+                if (WG_QL == 0) L.t[k] = v;
             }
             WG_SYNC();
             }
