@@ -203,5 +203,10 @@ case "$1" in
   s47) # Iter0 bookkeeping with batched loads and a parallel fold; the fused loop's last copies stored by its tail kernel
        $J "test:tests" && $J "bench:r05_s47_bench:$H" "bench:r05_s47_bench2:$H" "bench:r05_s47_1m:$M" "bench:r05_s47_c3s8:$S8" \
           "prof:r05_s47_prof:$H --ar-probe 0" ;;
+  s48) # workgroup refinement: thread groups per active row / factor row as wide as the active rows allow (DPP group
+       # sums) -- measured slower (rows / solve clocks 199 / 210 -> 215 / 231 Mcycles) and reverted
+       $J "test:tests/test_sslp.py tests/test_bench_settings.py tests/test_trajectories.py tests/test_gpu_parity.py tests/test_wg_blk.py" \
+          "bench:r05_s48_c2:--only C2 $A" "bench:r05_s48_c5a:--only C5a $A" "bench:r05_s48_c2b:--only C2 $A" && \
+       PHX_WG_PROF=1 $J "bench:r05_s48_c2_wgprof:--only C2 $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
