@@ -23,3 +23,4 @@ mv $P/r05_final_prof_kernel_stats.csv $P/r05_final_headline_kernel_stats.csv 2>/
 cp $G/r05_final_default.log $P/r05_final_bench_default.log
 cp $G/r05_final_default_detail.json $P/r05_final_bench_default_detail.json
 cp $G/test_1.log $P/r05_final_pytest_gpu_all.log 2>/dev/null || true
+cp $G/r05_final_smoke.log $P/r05_final_smoke.log 2>/dev/null || true

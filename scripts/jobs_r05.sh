@@ -104,7 +104,7 @@ case "$1" in
        PHX_SP_SPLIT=2 $J "test:tests/test_netdes.py" "bench:r05_s27_c5b_split2:--only C5b $A" && \
        $J "bench:r05_s27_c5b:--only C5b $A" ;;
   final) # the round's evidence: the whole GPU suite, the driver's default command, kernel traces
-       $J "test:tests" && $J "bench:r05_final_default:--detail gpurun_out/r05_final_default_detail.json" \
+       $J "test:tests" && $J "py:r05_final_smoke:scripts/run_smoke.py" "bench:r05_final_default:--detail gpurun_out/r05_final_default_detail.json" \
           "prof:r05_final_prof:$H --ar-probe 0" "prof:r05_final_c3s8_prof:$S8" "prof:r05_final_1m_prof:$M" \
           "prof:r05_final_c2_prof:--only C2 $A" "prof:r05_final_c4_prof:--only C4 $A" "prof:r05_final_c5a_prof:--only C5a $A" \
           "prof:r05_final_c5b_prof:--only C5b $A" ;;
