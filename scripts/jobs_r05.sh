@@ -208,5 +208,8 @@ case "$1" in
        $J "test:tests/test_sslp.py tests/test_bench_settings.py tests/test_trajectories.py tests/test_gpu_parity.py tests/test_wg_blk.py" \
           "bench:r05_s48_c2:--only C2 $A" "bench:r05_s48_c5a:--only C5a $A" "bench:r05_s48_c2b:--only C2 $A" && \
        PHX_WG_PROF=1 $J "bench:r05_s48_c2_wgprof:--only C2 $A" ;;
+  s49) # deferred Iter0 without statistics / completion markers (ev_run recorded at the finish; adoption needs none)
+       $J "test:tests" && $J "bench:r05_s49_bench:$H" "bench:r05_s49_bench2:$H" "bench:r05_s49_c3s8:$S8" \
+          "prof:r05_s49_prof:$H --ar-probe 0" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
