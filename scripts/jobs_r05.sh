@@ -211,5 +211,8 @@ case "$1" in
   s49) # deferred Iter0 without statistics / completion markers (ev_run recorded at the finish; adoption needs none)
        $J "test:tests" && $J "bench:r05_s49_bench:$H" "bench:r05_s49_bench2:$H" "bench:r05_s49_c3s8:$S8" \
           "prof:r05_s49_prof:$H --ar-probe 0" ;;
+  s50) # Iter0's pass counts stored into mapped host memory by a small kernel instead of a blit copy -- the same time
+       # (the kernel 4.5 us, then the same 5.8 us gap before the next: the host-memory writes' release), reverted
+       $J "test:tests" && $J "bench:r05_s50_bench:$H" "bench:r05_s50_bench2:$H" "prof:r05_s50_prof:$H --ar-probe 0" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
