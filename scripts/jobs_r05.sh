@@ -214,5 +214,8 @@ case "$1" in
   s50) # Iter0's pass counts stored into mapped host memory by a small kernel instead of a blit copy -- the same time
        # (the kernel 4.5 us, then the same 5.8 us gap before the next: the host-memory writes' release), reverted
        $J "test:tests" && $J "bench:r05_s50_bench:$H" "bench:r05_s50_bench2:$H" "prof:r05_s50_prof:$H --ar-probe 0" ;;
+  s51) # the timed object built before the warmup (the warmup's steps right before the timed region) against after it
+       $J "bench:r05_s51_new1:$H" "bench:r05_s51_old1:$H --build-after-warmup" "bench:r05_s51_new2:$H" \
+          "bench:r05_s51_old2:$H --build-after-warmup" "bench:r05_s51_new3:$H" "bench:r05_s51_old3:$H --build-after-warmup" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
