@@ -158,9 +158,12 @@ def _check(res, ncyl, tol=1e-9):
     ef, _, _ = oph.solve_ef([om.farmer("scen%d" % i, num_scens=S) for i in range(S)])
     assert h0["best_outer"] >= h0["trivial"] - 1e-9
     assert h0["best_outer"] <= ef + 1e-6 * abs(ef)
-    # (the hub sees the values it happened to read: not every bound the spoke wrote)
-    assert h0["best_outer"] in bounds + [h0["trivial"]]
-    assert h0["best_outer"] <= max(bounds + [h0["trivial"]])
+    # (the hub sees the values it happened to read: not every bound the spoke wrote;
+    # it may read the final pass's, computed on the kill buffer's zeros -- a trivial
+    # bound from a warm-started solve, equal to the trivial one to rounding)
+    written = [b for _, b, _ in g0]
+    assert h0["best_outer"] in written + [h0["trivial"]]
+    assert h0["best_outer"] <= max(written + [h0["trivial"]])
     assert h0["best_inner"] == float("inf")
     return [b for b in bounds]
 
