@@ -217,5 +217,7 @@ case "$1" in
   s51) # the timed object built before the warmup (the warmup's steps right before the timed region) against after it
        $J "bench:r05_s51_new1:$H" "bench:r05_s51_old1:$H --build-after-warmup" "bench:r05_s51_new2:$H" \
           "bench:r05_s51_old2:$H --build-after-warmup" "bench:r05_s51_new3:$H" "bench:r05_s51_old3:$H --build-after-warmup" ;;
+  s52) # final evidence on the final sources: the whole GPU suite, then the driver's default command
+       $J "test:tests" && $J "bench:r05_s52_default:--detail gpurun_out/r05_s52_default_detail.json" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
