@@ -36,16 +36,27 @@ class Comm:
     def Get_size(self):
         return self.size
 
-    def allreduce_(self, t):
-        """In-place SUM over ranks of a torch tensor (no-op on one rank)."""
-        if self.size > 1:
-            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+    def _reduce(self, t, op):
+        if self.size == 1:
+            return t
+        if t.is_cuda and self.backend != "nccl":
+            # gloo over device tensors (several ranks sharing one GPU, the
+            # multi-rank GPU tests): staged through the host -- the read-back
+            # waits on the current stream for the kernels that produced t, and
+            # the result is written back in that stream's order
+            h = t.cpu()
+            dist.all_reduce(h, op=op, group=self.group)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, op=op, group=self.group)
         return t
 
+    def allreduce_(self, t):
+        """In-place SUM over ranks of a torch tensor (no-op on one rank)."""
+        return self._reduce(t, dist.ReduceOp.SUM)
+
     def allreduce_max_(self, t):
-        if self.size > 1:
-            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
-        return t
+        return self._reduce(t, dist.ReduceOp.MAX)
 
     def Barrier(self):
         if self.size > 1:

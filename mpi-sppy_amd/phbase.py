@@ -585,6 +585,9 @@ class PHBase(SPOpt):
                         s = ext.get(stream)
                         if s is None:
                             s = ext[stream] = torch.cuda.ExternalStream(stream, device=dev)
+                        # (gloo: Comm.allreduce_ stages through the host -- a blocking
+                        # read-back on this stream, the host all-reduce, the result
+                        # written back in stream order)
                         with torch.cuda.stream(s):
                             comm.allreduce_(bufs[ptr][:count])
                     else:

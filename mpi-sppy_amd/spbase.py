@@ -349,7 +349,12 @@ class SPBase:
         lo, hi = self._local_lo, self._local_hi
         self._conv_R = R
         self._conv_counts = np.array([(b - a) * nn.N for a, b in vb], dtype=np.float64)
-        self._conv_seg = [(max(a, lo) - lo, max(min(b, hi), max(a, lo)) - lo) for a, b in vb]
+        # (each emulated rank's scenarios clipped to this rank's slice, in local
+        # indices; an emulated rank outside the slice is an empty segment inside it)
+        def clip(a, b):
+            a = min(max(a, lo), hi)
+            return a - lo, max(min(b, hi), a) - lo
+        self._conv_seg = [clip(a, b) for a, b in vb]
 
     # ------------------------------------------------------------ device
     def _t(self, a, dtype):

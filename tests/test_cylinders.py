@@ -97,7 +97,7 @@ def _worker(rank, world, port, out, gpu=False):
 
 
 def _run(world, gpu=False):
-    mgr = mp.Manager()
+    mgr = mp.get_context("spawn").Manager()
     out = mgr.dict()
     mp.spawn(_worker, args=(world, _free_port(), out, gpu), nprocs=world, join=True)
     return [out[r] for r in range(world)]
@@ -237,7 +237,7 @@ def test_wheel_three_cylinders_gap(emu):
     inner bound is the oracle's evaluation of x-bar (nonants fixed, LPs
     re-solved) of the nonant vector it came from; outer <= EF <= inner."""
     from oracle import models as om, ph as oph
-    mgr = mp.Manager()
+    mgr = mp.get_context("spawn").Manager()
     out = mgr.dict()
     mp.spawn(_worker3, args=(3, _free_port(), out), nprocs=3, join=True)
     res = [out[r] for r in range(3)]

@@ -60,7 +60,7 @@ def test_ranks_match_one(emu, case):
     from helpers import run_engine
     from mpisppy_amd.examples import aircond, farmer
     from mpisppy_amd.utils import sputils
-    mgr = mp.Manager()
+    mgr = mp.get_context("spawn").Manager()
     out = mgr.dict()
     world = 3 if case.startswith("aircond3") else 2
     mp.spawn(_worker, args=(world, _free_port(), out, case), nprocs=world, join=True)
@@ -128,7 +128,7 @@ def test_infeasible_deferred_iter0_two_ranks(emu):
     infeasible scenario on ONE rank: the stop decision is all-reduced, so both
     ranks leave the device loop before any PH iteration and quit together
     (phbase.py:812-823) instead of one rank waiting in iteration 1's all-reduce."""
-    mgr = mp.Manager()
+    mgr = mp.get_context("spawn").Manager()
     out = mgr.dict()
     mp.spawn(_worker_infeasible, args=(2, _free_port(), out), nprocs=2, join=True)
     for r in range(2):
