@@ -43,6 +43,8 @@ def test_bench_line_compact_cpu(tmp_path):
         assert k in d, k
     assert d["roofline"]["kernel"] and "frac" in d["roofline"] and "traffic_ratio" in d["roofline"]
     assert d["cpu_baseline"]["value"] > 0 and d["cpu_baseline"]["cores"] == 2
+    sp = d["cpu_baseline"]["spread"]                 # median of three samples, with their range
+    assert sp["samples"] == 3 and sp["min"] <= d["cpu_baseline"]["value"] <= sp["max"]
     for nm in ("C1", "C4"):
         c = d["configs"][nm]
         assert "error" not in c, c
@@ -61,3 +63,26 @@ def test_bench_launches_ranks_cpu():
     a, b = one["final"], two["final"]
     assert np.allclose(a["xbar"]["ROOT"], b["xbar"]["ROOT"], rtol=1e-12, atol=1e-12)
     assert abs(a["trivial_bound"] - b["trivial_bound"]) <= 1e-12 * abs(a["trivial_bound"])
+
+
+def test_compact_line_cap_cpu():
+    """whatever the record holds (long error strings, long CPU sample
+    text, many configs), the compact line fits LINE_CAP and keeps the contract keys."""
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bm = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bm)
+    big = "x" * 20000
+    res = {"metric": "m", "value": 1.0, "unit": "u", "n_gpus": 1, "steps": 2, "warmup": 1, "ms_per_step": 1.0,
+           "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": big,
+           "config": {"workload": big}, "roofline": {"kernel": "k", "frac": 0.1, "traffic_ratio": 1.0},
+           "cpu_baseline": {"value": 1.0, "unit": "u", "cores": 1, "kind": "port", "sample": big,
+                            "whole_host": {"value": 2.0, "how": big, "cap": big},
+                            "spread": {"samples": 3, "min": 0.9, "max": 1.1}},
+           "configs": {"C%d" % i: {"error": big} for i in range(200)}}
+    out = bm.compact_line(res, "detail.json")
+    line = json.dumps(out)
+    assert len(line.encode()) <= bm.LINE_CAP
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "roofline", "cpu_baseline"):
+        assert k in out, k

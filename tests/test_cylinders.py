@@ -162,7 +162,10 @@ def _check(res, ncyl, tol=1e-9):
     # it may read the final pass's, computed on the kill buffer's zeros -- a trivial
     # bound from a warm-started solve, equal to the trivial one to rounding)
     written = [b for _, b, _ in g0]
-    assert h0["best_outer"] in written + [h0["trivial"]]
+    # the final pass (kill buffer, W = 0, prox off) is the Iter0 problem again: its
+    # bound is the trivial bound (the one unchecked value the hub may read)
+    assert g0[-1][1] == pytest.approx(h0["trivial"], rel=1e-9)
+    assert h0["best_outer"] in bounds + [g0[-1][1], h0["trivial"]]
     assert h0["best_outer"] <= max(written + [h0["trivial"]])
     assert h0["best_inner"] == float("inf")
     return [b for b in bounds]

@@ -435,6 +435,33 @@ def test_native_loop_workgroup_stragglers_gpu(gpu_lib, ipm_cut):
         assert a.iterk_stats["straggler_stops"] == 0
 
 
+def test_wg_first_budget_after_gated_pass_gpu(gpu_lib):
+    """the first warm workgroup pass's round budget (wg_first) belongs
+    to the first pass that RUNS after a cold solve.  A device loop that stops at
+    iteration 1 (converged: its pass enqueued, gated, never run) gives the budget
+    back, so a second loop call's first pass gets wg_first as the host loop's
+    does; then a straggler-stopping loop (the sparse interior point cut short).
+    Both continuations equal the host loop's bit for bit."""
+    runs = []
+    for nl in (1, 0):
+        so = {"wg_warm": 8, "wg_first": 1, "ipm_max_it": 2, "native_loop": nl}
+        opts = ph_options(4, convthresh=1e9)
+        opts["iter0_solver_options"] = {"wg_warm": 8, "wg_first": 1}
+        opts["iterk_solver_options"] = so
+        ph = PH(opts, farmer.scenario_names_creator(120), farmer.scenario_creator,
+                scenario_creator_kwargs={"num_scens": 120, "crops_multiplier": 10}, _native_lib=gpu_lib)
+        ph.ph_main(finalize=False)
+        assert ph._PHIter == 1                  # converged at iteration 1: no solve ran
+        ph.options["convthresh"] = 1e-10
+        ph.iterk_loop()
+        ph._settle()
+        runs.append(ph)
+    a, b = runs
+    assert a.iterk_stats["iters"] == 4 and not hasattr(b, "iterk_stats")
+    assert np.array_equal(a.W_array(), b.W_array())
+    assert np.array_equal(a.nonant_values(), b.nonant_values())
+
+
 def test_sp_off_on_sparse_context_raises_gpu(gpu_lib):
     """sp = 0 (the dense generic path) on a context that holds the sparse
     solver's workspaces only: refused with an error, not run on absent buffers."""
