@@ -303,7 +303,7 @@ inline std::string lane_kernel_source(const LaneStructure& L, int warm_waves = 1
     // ... two waves per SIMD with every round on register data (above one
     // wavefront per SIMD; the compiler spills what does not fit 256 registers)
     o << "extern \"C\" __global__ void __launch_bounds__(64, 2) phx_lane_warm_fzr2(phx_lane::LaneIO io) {\n"
-         "  phx_lane::warm_fused<PT, true, PHX_FZR2_CARRY_DEF>(io);\n"
+         "  phx_lane::warm_fused<PT, true, PHX_FZR2_CARRY_DEF, PHX_FZR2_PARK_DEF>(io);\n"
          "}\n";
     // ... compacting: round 0 per lane, the later rounds of the lanes that need
     // them packed into full wavefronts by each group's last block (phx_lane.h

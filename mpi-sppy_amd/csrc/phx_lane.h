@@ -83,6 +83,13 @@ typedef unsigned long long uint64_t;
 #else
 #define PHX_FZR2_CARRY_DEF false
 #endif
+// The two-wave fused build parks its round data in LDS (warm_fused PARK);
+// PHX_FZR2_NO_PARK keeps them in registers (the round-5 build, 144 B of spill)
+#ifdef PHX_FZR2_NO_PARK
+#define PHX_FZR2_PARK_DEF false
+#else
+#define PHX_FZR2_PARK_DEF true
+#endif
 
 // Diagnostics hook (the CPU emulation defines it to record why a lane failed;
 // a no-op in the GPU kernels).
@@ -264,6 +271,35 @@ __device__ __forceinline__ void lane_stamp(const LaneIO& io, int k) {
 // at once (one scalar load; the counters stay as the last real solve left them)
 PHX_LD bool gated(const int32_t* gate) { return gate && *(const volatile int32_t*)gate; }
 
+// Hide a value's origin from the optimiser (no instruction): values derived
+// from it are recomputed where used instead of kept live across a loop.
+PHX_LD void opaque(double& v) {
+#if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC_RTC__)
+    __asm__ volatile("" : "+v"(v));
+#else
+    (void)v;
+#endif
+}
+PHX_LD int opaque_index(int v) {
+#if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC_RTC__)
+    __asm__ volatile("" : "+v"(v));
+#endif
+    return v;
+}
+// (an unsigned word likewise: bit masks read per use inside a loop)
+PHX_LD uint32_t opaque_u32(uint32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC_RTC__)
+    __asm__ volatile("" : "+v"(v));
+#endif
+    return v;
+}
+PHX_LD uint64_t opaque_u32(uint64_t v) {
+#if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC_RTC__)
+    __asm__ volatile("" : "+v"(v));
+#endif
+    return v;
+}
+
 // Data access for one lane: scenario-varying numbers in registers; the
 // invariant ones are literals of the specialised kernel (PT tables), which the
 // compiler rematerialises with scalar moves instead of keeping them live.
@@ -322,6 +358,28 @@ struct Data {
             pn[t] = r;
             kn += 0.5 * r * xb * xb;
         }
+    }
+    // A copy parked in LDS (park(): [av | qn | pn | kn] by lane, stride 64) and
+    // read back through an index the optimiser cannot see through: the same
+    // values as the Data that was parked, re-read where a round needs them
+    // instead of held live across the round loop (phx_lane_warm_fzr2)
+    static constexpr int PARK = PT::NMAX_V + 2 * PT::NMAX_S + 1;
+    PHX_LD Data(const LaneIO& io_, int sc_, const double* lds, int lane) : io(io_), sc(sc_) {
+        const int l = opaque_index(lane);
+        PHX_UNROLL for (int v = 0; v < PT::nvar(); ++v) av[v] = lds[v * 64 + l];
+        PHX_UNROLL for (int t = 0; t < PT::nslot(); ++t) {
+            qn[t] = lds[(PT::NMAX_V + t) * 64 + l];
+            pn[t] = lds[(PT::NMAX_V + PT::NMAX_S + t) * 64 + l];
+        }
+        kn = lds[(PT::NMAX_V + 2 * PT::NMAX_S) * 64 + l];
+    }
+    PHX_LD void park(double* lds, int lane) const {
+        PHX_UNROLL for (int v = 0; v < PT::nvar(); ++v) lds[v * 64 + lane] = av[v];
+        PHX_UNROLL for (int t = 0; t < PT::nslot(); ++t) {
+            lds[(PT::NMAX_V + t) * 64 + lane] = qn[t];
+            lds[(PT::NMAX_V + PT::NMAX_S + t) * 64 + lane] = pn[t];
+        }
+        lds[(PT::NMAX_V + 2 * PT::NMAX_S) * 64 + lane] = kn;
     }
     PHX_LD double A(int k) const { return PT::kvar(k) < 0 ? PT::Ac(k) : av[PT::kvar(k)]; }
     // scaling of the problem the lane solver works on (1 when unscaled)
@@ -536,21 +594,6 @@ PHX_LD bool row_free(int i) { return !PT::blfin(i) && !PT::bufin(i); }
 // (da = affine step of the slack's variable, 0 in the predictor pass).
 // Returns the relative KKT error of (x, y); *its = iterations used.
 // ---------------------------------------------------------------------------
-// Hide a value's origin from the optimiser (no instruction): values derived
-// from it are recomputed where used instead of kept live across a loop.
-PHX_LD void opaque(double& v) {
-#if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC_RTC__)
-    __asm__ volatile("" : "+v"(v));
-#else
-    (void)v;
-#endif
-}
-PHX_LD int opaque_index(int v) {
-#if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC_RTC__)
-    __asm__ volatile("" : "+v"(v));
-#endif
-    return v;
-}
 
 PHX_LD double comp_lo(double sl, double r, double z, double smu, double da) {
     return smu - sl * z + da * z * (sl + da) * r;
@@ -867,7 +910,9 @@ template <class PT>
 struct AMul {
     double fF[PT::NMAX_N];   // 1: column free
     double rR[PT::NMAX_M];   // 1: row active
-    PHX_LD explicit AMul(const ASet<PT>& a) {
+    typename ASet<PT>::CMask fb;   // the same as bit words (kkt_refine's LEAN steps)
+    uint32_t rb;
+    PHX_LD explicit AMul(const ASet<PT>& a) : fb(a.f), rb(a.r) {
         PHX_UNROLL for (int j = 0; j < PT::n(); ++j) fF[j] = bitd(a.f, j);
         PHX_UNROLL for (int i = 0; i < PT::m(); ++i) rR[i] = bitd(a.r, i);
     }
@@ -1042,7 +1087,11 @@ PHX_LD void col_residual(const Data<PT>& D, const RHS& R, const double* xp, cons
         g[j] = (PT::col_slot(j) >= 0 ? -R.q(j) - D.p(j) * xp[j] : -R.q(j)) - atz[j];
 }
 
-template <class PT, class RHS, bool CARRY = PHX_CARRY_DEF>
+// LEAN (the two-wave fused build): the free-column and active-row multipliers
+// of each step from the active set's bit words (read through an opaque copy
+// per step) instead of 19 doubles held live across the steps -- the same
+// values, so the same bits; 44 -> 20 B of scratch per lane there (offline ISA)
+template <class PT, class RHS, bool CARRY = PHX_CARRY_DEF, bool LEAN = false>
 PHX_LD void kkt_refine(const Data<PT>& D, const AMul<PT>& am, const KFactor<PT>& K, const RHS& R, double* xp,
                        double* z) {
     constexpr int NN = PT::NMAX_N, MM = PT::NMAX_M;
@@ -1073,20 +1122,24 @@ PHX_LD void kkt_refine(const Data<PT>& D, const AMul<PT>& am, const KFactor<PT>&
     PHX_REFINE_LOOP for (int it = 0; it < KKT_REFINE; ++it) {
         if (!CARRY) col_residual<PT>(D, R, xp, z, g);
         double t[MM];
+        const auto fbo = opaque_u32(am.fb);
+        const uint32_t rbo = opaque_u32(am.rb);
+        auto hfj = [&](int j) -> double { return LEAN ? bitd(fbo, j) * K.Hinv(j) : hf[j]; };
+        auto rRi = [&](int i) -> double { return LEAN ? bitd(rbo, i) : am.rR[i]; };
         {
             // t = A_R (xp + H_F g) - b_R: one mat-vec of the sum (the same
             // rounding as the two products it replaces, to eps |A| |x|)
             double u[NN], au[MM];
-            PHX_UNROLL for (int j = 0; j < PT::n(); ++j) u[j] = fma(g[j], hf[j], xp[j]);
+            PHX_UNROLL for (int j = 0; j < PT::n(); ++j) u[j] = fma(g[j], hfj(j), xp[j]);
             D.matvec(u, au);
-            PHX_UNROLL for (int i = 0; i < PT::m(); ++i) t[i] = am.rR[i] * (au[i] - bR[i]);
+            PHX_UNROLL for (int i = 0; i < PT::m(); ++i) t[i] = rRi(i) * (au[i] - bR[i]);
         }
         chol_solve_inv<PT>(K.M, t);   // inactive rows: identity, t stays 0
         double atdz[NN];
         D.matvec_t(t, atdz);
         double d2 = 0.0;
         PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
-            const double d = (g[j] - atdz[j]) * hf[j];
+            const double d = (g[j] - atdz[j]) * hfj(j);
             xp[j] += d;
             d2 += d * d;
             if (CARRY) g[j] = KKT_REG * d;
@@ -1174,7 +1227,7 @@ struct RhsSlot {      // d/dqn[t]: unit linear term on slot t's column, homogene
 // by its quasi-definite regularisation (P+reg, -reg) and iterative refinement
 // from the given (xp, z).  Non-free columns are set to their bound.  false if
 // the Schur complement is not positive definite.
-template <class PT, bool CARRY = PHX_CARRY_DEF>
+template <class PT, bool CARRY = PHX_CARRY_DEF, bool LEAN = false>
 PHX_LD bool kkt_solve(const Data<PT>& D, const ASet<PT>& a, double* xp, double* z) {
     KFactor<PT> K;
     const AMul<PT> am(a);
@@ -1195,7 +1248,7 @@ PHX_LD bool kkt_solve(const Data<PT>& D, const ASet<PT>& a, double* xp, double* 
         PHX_UNROLL for (int i = 0; i < PT::m(); ++i) { opaque(z[i]); z[i] = z0[i]; }
     }
 #endif
-    kkt_refine<PT, RhsFull<PT>, CARRY>(D, am, K, RhsFull<PT>{D, a}, xp, z);
+    kkt_refine<PT, RhsFull<PT>, CARRY, LEAN>(D, am, K, RhsFull<PT>{D, a}, xp, z);
     return true;
 }
 
@@ -1436,10 +1489,10 @@ PHX_LD void write_certified(const LaneIO& io, const Data<PT>& D, int sc, const A
 // One round with the given data: KKT solve, certificate, active-set update
 // (0 certified, 1 active set changed, 2 not certified and nothing to change,
 // 3 the Schur complement was not positive definite).
-template <class PT, bool CARRY = PHX_CARRY_DEF>
+template <class PT, bool CARRY = PHX_CARRY_DEF, bool LEAN = false>
 PHX_LD int as_round(const LaneIO& io, const Data<PT>& D, ASet<PT>& a, double* xp, double* z, int r) {
     PHX_LANE_STAT(0);
-    if (!kkt_solve<PT, CARRY>(D, a, xp, z)) return 3;
+    if (!kkt_solve<PT, CARRY, LEAN>(D, a, xp, z)) return 3;
     return certify_update<PT>(D, a, xp, z, io.kkt_tol, r >= io.single_after);
 }
 // r0: the index of the first round (the fused kernel runs round 0 itself)
@@ -2155,7 +2208,11 @@ __device__ __forceinline__ void compact_lane(bool still, int sc, int32_t* out, i
 // REG (the one-wave-per-SIMD build, 512 registers): every round runs on the
 // data in registers -- the other builds re-load it per round (kept live across
 // the round loop it spilled; a re-load is a memory round trip per round)
-template <class PT, bool REG = false, bool CARRY = PHX_CARRY_DEF>
+// PARK (with REG; the two-wave build): the round data parked in LDS after
+// round 0 and re-read per later round (Data::park), and the lean refinement
+// steps -- held in registers across the round loop they spilled 144 B per lane
+// (1.40x the kernel's algorithmic HBM bytes, r05); the same values, the same bits
+template <class PT, bool REG = false, bool CARRY = PHX_CARRY_DEF, bool PARK = false>
 __device__ __forceinline__ void warm_fused(const LaneIO& io) {
     const FusedW& f = io.fz;
     constexpr int NS = PT::nslot() > 0 ? PT::nslot() : 1;
@@ -2211,7 +2268,29 @@ __device__ __forceinline__ void warm_fused(const LaneIO& io) {
         // round 0 on the data in registers; later rounds re-load (as_rounds),
         // or with REG stay on them
         int c;
-        if (REG) {
+        if (REG && PARK) {
+            __shared__ double fz_park[Data<PT>::PARK * 64];
+            {
+                const Data<PT> D0(io, sc, av, wv, rv, xb);
+                D0.park(fz_park, threadIdx.x);
+                c = io.warm_rounds > 0 ? as_round<PT, CARRY, true>(io, D0, a, xp, z, 0) : 2;
+            }
+            int nr = 1;
+            PHX_NOUNROLL for (int r = 1; r < io.warm_rounds && c == 1; ++r, ++nr) {
+                const Data<PT> Dr(io, sc, fz_park, threadIdx.x);
+                c = as_round<PT, CARRY, true>(io, Dr, a, xp, z, r);
+            }
+            if (io.stamps) {
+                int wmax = 0;
+                for (int q = 1; q <= 8; ++q) wmax = __ballot(nr >= q) ? q : wmax;
+                if (threadIdx.x == 0) io.stamps[(uint64_t)blockIdx.x * 8 + 6] = (uint64_t)wmax;
+            }
+            if (c == 2) PHX_LANE_STAT(3);
+            if (c == 0) {
+                const Data<PT> Dw(io, sc, fz_park, threadIdx.x);
+                write_certified<PT>(io, Dw, sc, a, xp, z, 0);
+            }
+        } else if (REG) {
             const Data<PT> D0(io, sc, av, wv, rv, xb);
             c = io.warm_rounds > 0 ? as_round<PT, CARRY>(io, D0, a, xp, z, 0) : 2;
             int nr = 1;

@@ -1,0 +1,23 @@
+#!/bin/bash
+# Round-6 GPU evidence jobs (run through gpurun): bash scripts/jobs_r06.sh <name>.
+# Each job is a list of scripts/gpu_job.sh steps; logs land in gpurun_out/, the
+# summaries judged are copied into profiles/ (named after the job).
+set -o pipefail
+B="--configs none --no-cpu-baseline --no-conv --steps 50"                 # headline, K = 50
+H="--configs none --no-cpu-baseline --no-conv"                            # headline, K = 20 (driver shape)
+M="--only C3x1M --no-cpu-baseline --no-conv --steps 20 --warmup 1 --ar-probe 0"   # over-cache 1M
+A="--no-cpu-baseline --no-conv --steps 10 --warmup 1"                     # one secondary config
+S8="--only C3s8 --no-cpu-baseline --no-conv --steps 20"                   # the 8-GPU per-rank slice
+SQ="SQ_INSTS_VALU,SQ_ACTIVE_INST_VALU,SQ_WAVE_CYCLES,SQ_WAIT_ANY,SQ_INSTS_VALU_FLOPS_FP64,SQ_INSTS_SALU"
+NOPARK="PHX_LANE_DEFS=PHX_FZR2_NO_PARK"
+J="bash scripts/gpu_job.sh"
+case "$1" in
+  s8)  # the two-wave fused build with its round data parked in LDS (no spill): parity, then A/B against the
+       # round-5 build (same box, alternating), kernel trace, PMC bytes
+       $J "test:tests/test_gpu_parity.py tests/test_trajectories.py tests/test_bench_settings.py" && \
+       $J "bench:r06_s8_h1:$H --ar-probe 0" && env $NOPARK $J "bench:r06_s8_h1_nopark:$H --ar-probe 0" && \
+       $J "bench:r06_s8_h2:$H --ar-probe 0" && env $NOPARK $J "bench:r06_s8_h2_nopark:$H --ar-probe 0" && \
+       $J "bench:r06_s8_1m:$M" && env $NOPARK $J "bench:r06_s8_1m_nopark:$M" && \
+       $J "prof:r06_s8_prof:$H --ar-probe 0" "pmc:r06_pmc_c3_fetch:FETCH_SIZE:$B" "pmc:r06_pmc_c3_write:WRITE_SIZE:$B" ;;
+  *) echo "unknown job $1"; exit 2 ;;
+esac
