@@ -187,6 +187,11 @@ typedef struct phx_tree_desc {
     int32_t npart;             /* size of the partial buffer (doubles)        */
     int32_t nnodes_cover;      /* sum of node_nlen over the local nodes (== NNS
                                   when every node has a local scenario)       */
+    const int32_t* node_key;   /* [N][S] optional (may be NULL): the node-slot
+                                  index of each (nonant slot, local scenario),
+                                  the x-bar index of phx_update_w.  With it,
+                                  small batches (S <= 1024) take phx_xbar /
+                                  phx_update_w / phx_iterk's one-block path   */
 } phx_tree_desc;
 
 /* ---- lifetime ---------------------------------------------------------- */

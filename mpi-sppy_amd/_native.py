@@ -68,6 +68,7 @@ class TreeDesc(ctypes.Structure):
         ("nnodes", c_int32),
         ("node_tile_ptr", c_void_p), ("node_off", c_void_p), ("node_nlen", c_void_p),
         ("NNS", c_int32), ("npart", c_int32), ("nnodes_cover", c_int32),
+        ("node_key", c_void_p),
     ]
 
 

@@ -1377,6 +1377,54 @@ PHX_LD int worst_violation(const Data<PT>& D, CM enter_lo, CM enter_up, CM leave
 #endif
 }
 
+#ifdef PHX_MULTI_THETA
+// (experiment) the flagged changes whose relative violation is at least theta
+// times the largest one (worst_violation's measures): a bounded update between
+// the full primal-dual update and a single change
+template <class PT, class CM>
+PHX_LD void multi_violations(const Data<PT>& D, CM& enter_lo, CM& enter_up, CM& leave, uint32_t& act_lo,
+                             uint32_t& act_up, uint32_t& drop, const double* xp, const double* z, double qmax,
+                             double theta) {
+    const double idt = 1.0 / (1.0 + qmax);
+    double atz[PT::NMAX_N], axp[PT::NMAX_M];
+    D.matvec_t(z, atz);
+    D.matvec(xp, axp);
+    double vlo[PT::NMAX_N], vup[PT::NMAX_N], vlv[PT::NMAX_N], rlo[PT::NMAX_M], rup[PT::NMAX_M], rdr[PT::NMAX_M];
+    double mx = 0.0;
+    PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
+        const double d = D.dc(j);
+        const double lam = (D.qpx(j, xp[j]) + atz[j]) * D.idc(j);
+        vlo[j] = vup[j] = -1.0;
+        if (PT::lfin(j) && ((enter_lo >> j) & 1)) vlo[j] = (D.l(j) - xp[j]) * d / (1.0 + fabs(D.l(j) * d));
+        if (PT::ufin(j) && ((enter_up >> j) & 1)) vup[j] = (xp[j] - D.u(j)) * d / (1.0 + fabs(D.u(j) * d));
+        vlv[j] = ((leave >> j) & 1) ? fabs(lam) * idt : -1.0;
+        mx = fmax(mx, fmax(vlo[j], fmax(vup[j], vlv[j])));
+    }
+    PHX_UNROLL for (int i = 0; i < PT::m(); ++i) {
+        const double id = D.idr(i);
+        rlo[i] = rup[i] = -1.0;
+        if (PT::blfin(i) && ((act_lo >> i) & 1u)) rlo[i] = (D.bl(i) - axp[i]) * id / (1.0 + fabs(D.bl(i) * id));
+        if (PT::bufin(i) && ((act_up >> i) & 1u)) rup[i] = (axp[i] - D.bu(i)) * id / (1.0 + fabs(D.bu(i) * id));
+        rdr[i] = ((drop >> i) & 1u) ? fabs(z[i] * D.dr(i)) * idt : -1.0;
+        mx = fmax(mx, fmax(rlo[i], fmax(rup[i], rdr[i])));
+    }
+    const double cut = theta * mx;
+    CM el = 0, eu = 0, lv = 0;
+    uint32_t al = 0, au = 0, dr = 0;
+    PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
+        el |= (CM)(vlo[j] >= cut && vlo[j] >= 0.0) << j;
+        eu |= (CM)(vup[j] >= cut && vup[j] >= 0.0) << j;
+        lv |= (CM)(vlv[j] >= cut && vlv[j] >= 0.0) << j;
+    }
+    PHX_UNROLL for (int i = 0; i < PT::m(); ++i) {
+        al |= (uint32_t)(rlo[i] >= cut && rlo[i] >= 0.0) << i;
+        au |= (uint32_t)(rup[i] >= cut && rup[i] >= 0.0) << i;
+        dr |= (uint32_t)(rdr[i] >= cut && rdr[i] >= 0.0) << i;
+    }
+    enter_lo = el; enter_up = eu; leave = lv; act_lo = al; act_up = au; drop = dr;
+}
+#endif
+
 // KKT certificate of (xp, z) for active set a (unscaled, relative kkt_tol);
 // on failure applies the primal-dual active-set update (violated bounds/rows
 // enter, wrong-signed multipliers leave).  Returns 0 certified, 1 active set
@@ -1387,7 +1435,7 @@ PHX_LD int worst_violation(const Data<PT>& D, CM enter_lo, CM enter_up, CM leave
 // degenerate LP faces, one change at a time walks them like a pivot.
 template <class PT>
 PHX_LD int certify_update(const Data<PT>& D, ASet<PT>& a, const double* xp, const double* z, double kkt_tol,
-                          bool single = false) {
+                          bool single = false, bool multi = false) {
     typedef typename ASet<PT>::CMask CM;
     double qmax = 0.0;
     PHX_UNROLL for (int j = 0; j < PT::n(); ++j) qmax = fmax(qmax, fabs(D.q(j) * D.idc(j)));
@@ -1450,6 +1498,13 @@ PHX_LD int certify_update(const Data<PT>& D, ASet<PT>& a, const double* xp, cons
     }
     if (!(fin == 0.0)) return 2;      // not certified, and no update can repair it
     const bool changed = (enter_lo | enter_up | leave) != 0 || (act_lo | act_up | drop) != 0;
+#ifdef PHX_MULTI_THETA
+    if (multi && changed) {
+        multi_violations<PT>(D, enter_lo, enter_up, leave, act_lo, act_up, drop, xp, z, qmax, PHX_MULTI_THETA);
+    } else
+#else
+    (void)multi;
+#endif
     if (single && changed) {
         // (the rare path: the violations' sizes are recomputed here so the
         // common certificate carries none of this)
@@ -1493,7 +1548,13 @@ template <class PT, bool CARRY = PHX_CARRY_DEF, bool LEAN = false>
 PHX_LD int as_round(const LaneIO& io, const Data<PT>& D, ASet<PT>& a, double* xp, double* z, int r) {
     PHX_LANE_STAT(0);
     if (!kkt_solve<PT, CARRY, LEAN>(D, a, xp, z)) return 3;
+#ifdef PHX_MULTI_THETA
+    // (experiment) the first PHX_MULTI_ROUNDS rounds after single_after: bounded updates
+    return certify_update<PT>(D, a, xp, z, io.kkt_tol, r >= io.single_after,
+                              r >= io.single_after && r < io.single_after + PHX_MULTI_ROUNDS);
+#else
     return certify_update<PT>(D, a, xp, z, io.kkt_tol, r >= io.single_after);
+#endif
 }
 // r0: the index of the first round (the fused kernel runs round 0 itself)
 // (a certified lane is written by the caller from re-loaded data: writing it

@@ -468,6 +468,7 @@ class SPBase:
         tree.NNS = self.NNS
         tree.npart = o
         tree.nnodes_cover = int(sum(int(self._node_nlen[v]) for v in node_ids))
+        tree.node_key = self._xbar_idx_t.data_ptr()
         self._tree = tree
         self._tree_t = td
         segs = self._conv_seg

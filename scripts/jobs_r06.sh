@@ -19,5 +19,17 @@ case "$1" in
        $J "bench:r06_s8_h2:$H --ar-probe 0" && env $NOPARK $J "bench:r06_s8_h2_nopark:$H --ar-probe 0" && \
        $J "bench:r06_s8_1m:$M" && env $NOPARK $J "bench:r06_s8_1m_nopark:$M" && \
        $J "prof:r06_s8_prof:$H --ar-probe 0" "pmc:r06_pmc_c3_fetch:FETCH_SIZE:$B" "pmc:r06_pmc_c3_write:WRITE_SIZE:$B" ;;
+  s9)  # C4: Compute_Xbar + Update_W + convergence_diff of small batches in one block (k_small_xw): the whole
+       # suite, then C4 A/B against the two-kernel path (PHX_SMALL_XW=0), kernel trace
+       $J "test:tests" && \
+       $J "bench:r06_s9_c4:--only C4 $A" && PHX_SMALL_XW=0 $J "bench:r06_s9_c4_old:--only C4 $A" && \
+       $J "bench:r06_s9_c4b:--only C4 $A" && PHX_SMALL_XW=0 $J "bench:r06_s9_c4b_old:--only C4 $A" && \
+       $J "prof:r06_s9_c4_prof:--only C4 $A" ;;
+  s10) # k_small_xw with its run sums in LDS; C4 with the kernel timing in a run of its own (the default configs path)
+       $J "test:tests/test_gpu_parity.py tests/test_trajectories.py tests/test_distributed_gpu.py tests/test_hydro.py" && \
+       $J "bench:r06_s10_c4:--configs C4 --no-cpu-baseline --no-conv --ar-probe 0 --steps 10 --warmup 1" && \
+       PHX_SMALL_XW=0 $J "bench:r06_s10_c4_old:--configs C4 --no-cpu-baseline --no-conv --ar-probe 0 --steps 10 --warmup 1" && \
+       $J "bench:r06_s10_c4b:--configs C4 --no-cpu-baseline --no-conv --ar-probe 0 --steps 10 --warmup 1" && \
+       $J "prof:r06_s10_c4_prof:--only C4 $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
