@@ -31,5 +31,15 @@ case "$1" in
        PHX_SMALL_XW=0 $J "bench:r06_s10_c4_old:--configs C4 --no-cpu-baseline --no-conv --ar-probe 0 --steps 10 --warmup 1" && \
        $J "bench:r06_s10_c4b:--configs C4 --no-cpu-baseline --no-conv --ar-probe 0 --steps 10 --warmup 1" && \
        $J "prof:r06_s10_c4_prof:--only C4 $A" ;;
+  s11) # sparse configs: the split level 2 layout (four workgroups per CU) against the default, C5a / C5b; C5b's
+       # setup trace (the lazy PDHG step size: no k_norm)
+       Q="--configs C5a,C5b --no-cpu-baseline --no-conv --ar-probe 0 --steps 10 --warmup 1"
+       $J "bench:r06_s11_sp:$Q" && PHX_SP_SPLIT=2 $J "bench:r06_s11_sp_split2:$Q" && \
+       $J "prof:r06_s11_c5b_prof:--only C5b $A" ;;
+  s12) # the per-iteration glue kernels by element / slot chunk (k_begin_vec, k_ph_terms2, k_update_w_seg2, k_xbar's
+       # fold by slot), split level 2 for the sparse-primary problems: parity, C5a / C5b / C2, C5b trace
+       Q="--configs C2,C5a,C5b --no-cpu-baseline --no-conv --ar-probe 0 --steps 10 --warmup 1"
+       $J "test:tests/test_netdes.py tests/test_sslp.py tests/test_bench_settings.py tests/test_trajectories.py tests/test_gpu_parity.py" && \
+       $J "bench:r06_s12_sp:$Q" "prof:r06_s12_c5b_prof:--only C5b $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
