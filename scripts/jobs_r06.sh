@@ -41,5 +41,13 @@ case "$1" in
        Q="--configs C2,C5a,C5b --no-cpu-baseline --no-conv --ar-probe 0 --steps 10 --warmup 1"
        $J "test:tests/test_netdes.py tests/test_sslp.py tests/test_bench_settings.py tests/test_trajectories.py tests/test_gpu_parity.py" && \
        $J "bench:r06_s12_sp:$Q" "prof:r06_s12_c5b_prof:--only C5b $A" ;;
+  s13) # C5a / C2 kernel traces (where their steps go after the glue-kernel changes)
+       $J "prof:r06_s13_c5a_prof:--only C5a $A" "prof:r06_s13_c2_prof:--only C2 $A" ;;
+  s14) # the glue kernels by slot chunk from 16 slots (C2), the counters zeroed by the PH-terms kernel
+       Q="--configs C2,C5a,C5b --no-cpu-baseline --no-conv --ar-probe 0 --steps 10 --warmup 1"
+       $J "test:tests/test_netdes.py tests/test_sslp.py tests/test_bench_settings.py tests/test_trajectories.py tests/test_gpu_parity.py" && \
+       $J "bench:r06_s14_sp:$Q" "prof:r06_s14_c2_prof:--only C2 $A" ;;
+  s15) # the whole GPU suite, then the driver's default command
+       $J "test:tests" && $J "bench:r06_s15_default:--detail gpurun_out/r06_s15_default_detail.json" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
