@@ -49,5 +49,21 @@ case "$1" in
        $J "bench:r06_s14_sp:$Q" "prof:r06_s14_c2_prof:--only C2 $A" ;;
   s15) # the whole GPU suite, then the driver's default command
        $J "test:tests" && $J "bench:r06_s15_default:--detail gpurun_out/r06_s15_default_detail.json" ;;
+  s16) # the per-rank slice (C3s8) and the headline: kernel traces of the timed windows
+       $J "prof:r06_s16_c3s8_prof:$S8" "prof:r06_s16_prof:$H --ar-probe 0" ;;
+  final) # the round's evidence: the whole GPU suite, smoke, the driver's default command, kernel traces
+       $J "test:tests" && $J "py:r06_final_smoke:scripts/run_smoke.py" "bench:r06_final_default:--detail gpurun_out/r06_final_default_detail.json" \
+          "prof:r06_final_prof:$H --ar-probe 0" "prof:r06_final_c3s8_prof:$S8" "prof:r06_final_1m_prof:$M" \
+          "prof:r06_final_c2_prof:--only C2 $A" "prof:r06_final_c4_prof:--only C4 $A" "prof:r06_final_c5a_prof:--only C5a $A" \
+          "prof:r06_final_c5b_prof:--only C5b $A" ;;
+  pmc1) # PMC passes on the final kernels (one counter group per pass): the lane kernels
+       $J "pmc:r06_pmc_c3_fetch:FETCH_SIZE:$B" "pmc:r06_pmc_c3_write:WRITE_SIZE:$B" "pmc:r06_pmc_c3_sq:$SQ:$B" \
+          "pmc:r06_pmc_s8_fetch:FETCH_SIZE:$S8" "pmc:r06_pmc_s8_write:WRITE_SIZE:$S8" "pmc:r06_pmc_s8_sq:$SQ:$S8" \
+          "pmc:r06_pmc_1m_fetch:FETCH_SIZE:$M" "pmc:r06_pmc_1m_write:WRITE_SIZE:$M" \
+          "pmc:r06_pmc_c4_fetch:FETCH_SIZE:--only C4 $A" "pmc:r06_pmc_c4_write:WRITE_SIZE:--only C4 $A" ;;
+  pmc2) # ... the workgroup and sparse solvers
+       $J "pmc:r06_pmc_c2_fetch:FETCH_SIZE:--only C2 $A" "pmc:r06_pmc_c2_write:WRITE_SIZE:--only C2 $A" \
+          "pmc:r06_pmc_c5a_fetch:FETCH_SIZE:--only C5a $A" "pmc:r06_pmc_c5a_write:WRITE_SIZE:--only C5a $A" \
+          "pmc:r06_pmc_c5b_fetch:FETCH_SIZE:--only C5b $A" "pmc:r06_pmc_c5b_write:WRITE_SIZE:--only C5b $A" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
