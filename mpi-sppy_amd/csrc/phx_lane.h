@@ -619,6 +619,51 @@ PHX_LD void ipm_opaque(double* x, double* zl, double* zu, double* rl, double* ru
     }
 }
 
+// The interior point's per-iteration arrays read in both passes -- the normal
+// matrix's factor, the column and row scalings, the predictor's directions --
+// parked in LDS on the GPU (one wavefront per block, [slot][lane]) and read
+// back where they are used, through an index the optimiser cannot see
+// through: with them held in registers across the passes the iteration's
+// live set (farmer: ~340 VGPRs) overflowed into AGPRs, one accvgpr move per
+// 32-bit half per use (≈1,000 moves against ≈2,300 FP64 operations per
+// iteration, offline ISA).  The values read back are the values stored, so
+// the arithmetic is unchanged.  On only when the block fits 40 KB (one
+// wavefront per SIMD, four blocks per CU); PHX_IPM_NO_PARK keeps registers.
+#if (defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC_RTC__)) && !defined(PHX_IPM_NO_PARK)
+#define PHX_IPM_PARK_ON 1
+#else
+#define PHX_IPM_PARK_ON 0
+#endif
+template <class PT>
+struct IpmPark {
+    static constexpr int NN = PT::NMAX_N, MM = PT::NMAX_M, TT = PT::NMAX_M * (PT::NMAX_M + 1) / 2;
+    static constexpr int OM = 0, ODX = TT, OIS = TT + NN, ODXA = TT + NN + MM, ODSA = TT + 2 * NN + MM;
+    static constexpr int SIZE = TT + 2 * NN + 2 * MM;
+    static constexpr bool ON = PHX_IPM_PARK_ON && SIZE * 64 * 8 <= 40960;
+};
+template <class PT, int K>
+PHX_LD void ipm_put(double* lds, const double* v, int off) {
+    if (IpmPark<PT>::ON) {
+#if PHX_IPM_PARK_ON
+        const int l = threadIdx.x;
+        PHX_UNROLL for (int k = 0; k < K; ++k) lds[(off + k) * 64 + l] = v[k];
+#endif
+    }
+}
+template <class PT, int K>
+PHX_LD void ipm_get(const double* lds, double* v, int off) {
+    if (IpmPark<PT>::ON) {
+#if PHX_IPM_PARK_ON
+        const int l = opaque_index(threadIdx.x);
+        PHX_UNROLL for (int k = 0; k < K; ++k) v[k] = lds[(off + k) * 64 + l];
+#endif
+    }
+}
+
+#ifndef PHX_IPM_CHECK_FROM
+#define PHX_IPM_CHECK_FROM 6
+#endif
+
 // The start point's scales come from the problem (phx_jit.h: xs a fifth of
 // the median bound / row-side magnitude, ws half the median cost magnitude,
 // zs a tenth of ws); PHX_IPM_SCALES=0 (a JIT define) restores the unit
@@ -636,6 +681,12 @@ template <class PT>
 PHX_LD double ipm_core(const Data<PT>& D, int max_it, double tol, double* x, double* y, int* its,
                        double xs = PHX_IPM_XS_, double zs = PHX_IPM_ZS_, double ws = PHX_IPM_WS_) {
     constexpr int NN = PT::NMAX_N, MM = PT::NMAX_M, TT = PT::NMAX_M * (PT::NMAX_M + 1) / 2;
+    typedef IpmPark<PT> PK;
+#if PHX_IPM_PARK_ON
+    __shared__ double ipm_lds[PK::ON ? PK::SIZE * 64 : 1];
+#else
+    double* const ipm_lds = nullptr;
+#endif
     const double reg = 1e-10;
     double zl[NN], zu[NN], s[MM], wl[MM], wu[MM];
     // start point (cost-aware multipliers)
@@ -676,8 +727,13 @@ PHX_LD double ipm_core(const Data<PT>& D, int max_it, double tol, double* x, dou
     double err = 1e300;
     int it = 0;
     for (; it < max_it; ++it) {
-        err = D.kkt(x, y);
-        if (err < tol || !(err < 1e300)) break;
+        // (the KKT error from iteration PHX_IPM_CHECK_FROM on, and at the last
+        // one: no interior point converges in fewer, and the error of the
+        // start's first iterations is ~1/3 of an iteration's work)
+        if (it >= PHX_IPM_CHECK_FROM || it == max_it - 1) {
+            err = D.kkt(x, y);
+            if (err < tol || !(err < 1e300)) break;
+        }
         // reciprocal slacks
         double rl[NN], ru[NN], rwl[MM], rwu[MM];
         double mu = 0.0;
@@ -716,6 +772,9 @@ PHX_LD double ipm_core(const Data<PT>& D, int max_it, double tol, double* x, dou
                 M[PT::pair_pos(t)] += D.A(ka) * Dx[PT::col(ka)] * D.A(kb);
         }
         if (!cholesky_ipm<PT>(M)) { PHX_LANE_FAIL(20, it); break; }
+        ipm_put<PT, TT>(ipm_lds, M, PK::OM);
+        ipm_put<PT, NN>(ipm_lds, Dx, PK::ODX);
+        ipm_put<PT, MM>(ipm_lds, isig, PK::OIS);
         // predictor (pass 0, smu = 0) then corrector (pass 1)
         double smu = 0.0, ap = 1.0, ad = 1.0;
         double dx[NN], ds[MM], dy[MM], dxa[NN], dsa[MM];
@@ -723,6 +782,8 @@ PHX_LD double ipm_core(const Data<PT>& D, int max_it, double tol, double* x, dou
         PHX_UNROLL for (int i = 0; i < PT::m(); ++i) dsa[i] = 0.0;
         PHX_IPM_PASS_LOOP for (int pass = 0; pass < 2; ++pass) {
             ipm_opaque<PT>(x, zl, zu, rl, ru, s, wl, wu, rwl, rwu, y);
+            if (pass == 1) ipm_get<PT, NN>(ipm_lds, dxa, PK::ODXA);
+            ipm_get<PT, NN>(ipm_lds, Dx, PK::ODX);
             {
                 double ax[MM], aty[NN];
                 D.matvec(x, ax);
@@ -731,25 +792,27 @@ PHX_LD double ipm_core(const Data<PT>& D, int max_it, double tol, double* x, dou
                     double r = aty[j] - D.p(j) * x[j] - D.q(j);
                     if (has_lo<PT>(j)) {
                         const double sl = x[j] - D.l(j);
-                        r += zl[j] + comp_lo(sl, rl[j], zl[j], smu, dxa[j]) * rl[j];
+                        r += zl[j] + (pass == 0 ? -(sl * zl[j]) : comp_lo(sl, rl[j], zl[j], smu, dxa[j])) * rl[j];
                     }
                     if (has_up<PT>(j)) {
                         const double sl = D.u(j) - x[j];
-                        r -= zu[j] + comp_up(sl, ru[j], zu[j], smu, dxa[j]) * ru[j];
+                        r -= zu[j] + (pass == 0 ? -(sl * zu[j]) : comp_up(sl, ru[j], zu[j], smu, dxa[j])) * ru[j];
                     }
                     dx[j] = PT::fixed(j) ? 0.0 : r * Dx[j];      // H^-1 rho_x
                 }
                 double ahr[MM];
                 D.matvec(dx, ahr);
+                ipm_get<PT, MM>(ipm_lds, isig, PK::OIS);
+                if (pass == 1) ipm_get<PT, MM>(ipm_lds, dsa, PK::ODSA);
                 PHX_UNROLL for (int i = 0; i < PT::m(); ++i) {
                     double rhos = -y[i];
                     if (row_lo<PT>(i)) {
                         const double sl = s[i] - D.bl(i);
-                        rhos += wl[i] + comp_lo(sl, rwl[i], wl[i], smu, dsa[i]) * rwl[i];
+                        rhos += wl[i] + (pass == 0 ? -(sl * wl[i]) : comp_lo(sl, rwl[i], wl[i], smu, dsa[i])) * rwl[i];
                     }
                     if (row_up<PT>(i)) {
                         const double sl = D.bu(i) - s[i];
-                        rhos -= wu[i] + comp_up(sl, rwu[i], wu[i], smu, dsa[i]) * rwu[i];
+                        rhos -= wu[i] + (pass == 0 ? -(sl * wu[i]) : comp_up(sl, rwu[i], wu[i], smu, dsa[i])) * rwu[i];
                     }
                     ds[i] = rhos;
                     if (row_free<PT>(i)) dy[i] = 0.0;
@@ -757,45 +820,69 @@ PHX_LD double ipm_core(const Data<PT>& D, int max_it, double tol, double* x, dou
                     else dy[i] = -(ax[i] - s[i]) + rhos * isig[i] - ahr[i];
                 }
             }
+            ipm_get<PT, TT>(ipm_lds, M, PK::OM);
             chol_solve_inv<PT>(M, dy);
             {
                 double atdy[NN];
                 D.matvec_t(dy, atdy);
+                ipm_get<PT, NN>(ipm_lds, Dx, PK::ODX);
                 PHX_UNROLL for (int j = 0; j < PT::n(); ++j)
                     if (!PT::fixed(j)) dx[j] += Dx[j] * atdy[j];
             }
+            ipm_get<PT, MM>(ipm_lds, isig, PK::OIS);
             PHX_UNROLL for (int i = 0; i < PT::m(); ++i)
                 ds[i] = (PT::eq(i) || row_free<PT>(i)) ? 0.0 : (ds[i] - dy[i]) * isig[i];
             ipm_opaque<PT>(x, zl, zu, rl, ru, s, wl, wu, rwl, rwu, y);
             // step lengths as inverse ratios (step = 1 / max(1, max ratio)),
             // multiplier steps recomputed from dx, ds
             double apr = 1.0, adr = 1.0;
+            if (pass == 1) {
+                ipm_get<PT, NN>(ipm_lds, dxa, PK::ODXA);
+                ipm_get<PT, MM>(ipm_lds, dsa, PK::ODSA);
+            }
             PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
+                // (the predictor's comp = -sl z: -dz / z = (sl + dx) r, no reciprocal of z)
                 if (has_lo<PT>(j)) {
                     const double sl = x[j] - D.l(j);
-                    const double dz = (comp_lo(sl, rl[j], zl[j], smu, dxa[j]) - zl[j] * dx[j]) * rl[j];
                     apr = fmax(apr, -dx[j] * rl[j]);
-                    adr = fmax(adr, -dz * rcp_step(zl[j]));
+                    if (pass == 0) {
+                        adr = fmax(adr, (sl + dx[j]) * rl[j]);
+                    } else {
+                        const double dz = (comp_lo(sl, rl[j], zl[j], smu, dxa[j]) - zl[j] * dx[j]) * rl[j];
+                        adr = fmax(adr, -dz * rcp_step(zl[j]));
+                    }
                 }
                 if (has_up<PT>(j)) {
                     const double sl = D.u(j) - x[j];
-                    const double dz = (comp_up(sl, ru[j], zu[j], smu, dxa[j]) + zu[j] * dx[j]) * ru[j];
                     apr = fmax(apr, dx[j] * ru[j]);
-                    adr = fmax(adr, -dz * rcp_step(zu[j]));
+                    if (pass == 0) {
+                        adr = fmax(adr, (sl - dx[j]) * ru[j]);
+                    } else {
+                        const double dz = (comp_up(sl, ru[j], zu[j], smu, dxa[j]) + zu[j] * dx[j]) * ru[j];
+                        adr = fmax(adr, -dz * rcp_step(zu[j]));
+                    }
                 }
             }
             PHX_UNROLL for (int i = 0; i < PT::m(); ++i) {
                 if (row_lo<PT>(i)) {
                     const double sl = s[i] - D.bl(i);
-                    const double dw = (comp_lo(sl, rwl[i], wl[i], smu, dsa[i]) - wl[i] * ds[i]) * rwl[i];
                     apr = fmax(apr, -ds[i] * rwl[i]);
-                    adr = fmax(adr, -dw * rcp_step(wl[i]));
+                    if (pass == 0) {
+                        adr = fmax(adr, (sl + ds[i]) * rwl[i]);
+                    } else {
+                        const double dw = (comp_lo(sl, rwl[i], wl[i], smu, dsa[i]) - wl[i] * ds[i]) * rwl[i];
+                        adr = fmax(adr, -dw * rcp_step(wl[i]));
+                    }
                 }
                 if (row_up<PT>(i)) {
                     const double sl = D.bu(i) - s[i];
-                    const double dw = (comp_up(sl, rwu[i], wu[i], smu, dsa[i]) + wu[i] * ds[i]) * rwu[i];
                     apr = fmax(apr, ds[i] * rwu[i]);
-                    adr = fmax(adr, -dw * rcp_step(wu[i]));
+                    if (pass == 0) {
+                        adr = fmax(adr, (sl - ds[i]) * rwu[i]);
+                    } else {
+                        const double dw = (comp_up(sl, rwu[i], wu[i], smu, dsa[i]) + wu[i] * ds[i]) * rwu[i];
+                        adr = fmax(adr, -dw * rcp_step(wu[i]));
+                    }
                 }
             }
             ap = rcp_fast(apr);
@@ -831,11 +918,15 @@ PHX_LD double ipm_core(const Data<PT>& D, int max_it, double tol, double* x, dou
                 maff *= inv_ncomp;
                 const double ratio = mu > 0.0 ? maff / mu : 0.0;
                 smu = ratio * ratio * ratio * mu;
+                ipm_put<PT, NN>(ipm_lds, dxa, PK::ODXA);
+                ipm_put<PT, MM>(ipm_lds, dsa, PK::ODSA);
             }
         }
         // update (multipliers first: they use the old slacks)
         ap = fmin(1.0, 0.995 * ap);
         ad = fmin(1.0, 0.995 * ad);
+        ipm_get<PT, NN>(ipm_lds, dxa, PK::ODXA);
+        ipm_get<PT, MM>(ipm_lds, dsa, PK::ODSA);
         PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
             if (has_lo<PT>(j)) {
                 const double sl = x[j] - D.l(j);

@@ -31,7 +31,7 @@ from mpisppy_amd.opt.ph import PH
 lib = _native.Lib(%(so)r, prefix="emu_phx_")
 S, K = %(S)d, %(K)d
 opts = ph_options(K)
-opts["iterk_solver_options"] = {"native_loop": 0}
+opts["iterk_solver_options"] = dict({"native_loop": 0}, **dict(%(sok)s))
 opts["iter0_solver_options"] = dict(%(so0)s)
 ph = PH(opts, farmer.scenario_names_creator(S), farmer.scenario_creator, scenario_creator_kwargs={"num_scens": S},
         _native_lib=lib, _device="cpu")
@@ -49,7 +49,8 @@ def main():
     so = build(flags)
     env = dict(os.environ, PHX_EMU_DEBUG="1")
     so0 = os.environ.get("EMU_SO0", "{}")
-    r = subprocess.run([sys.executable, "-c", CHILD % {"root": _ROOT, "so": so, "S": S, "K": K, "so0": so0}],
+    sok = os.environ.get("EMU_SOK", "{}")      # iterk solver options (e.g. as_rounds)
+    r = subprocess.run([sys.executable, "-c", CHILD % {"root": _ROOT, "so": so, "S": S, "K": K, "so0": so0, "sok": sok}],
                        capture_output=True, text=True, env=env)
     k = 0
     for line in r.stderr.splitlines():

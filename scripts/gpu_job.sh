@@ -7,6 +7,7 @@
 #   trace:<tag>:<bench.py args>         rocprofv3 --kernel-trace --hip-runtime-trace (host gaps)
 #   pmc:<tag>:<counters>:<bench.py args> rocprofv3 --pmc (one pass; counters comma-separated)
 #   py:<tag>:<script and args>
+#   run:<tag>:<program and args>        (a prebuilt binary, e.g. scripts/micro/*)
 # Logs: gpurun_out/<tag>.log (tests: gpurun_out/test_<n>.log).
 set -o pipefail
 mkdir -p gpurun_out
@@ -47,6 +48,11 @@ for step in "$@"; do
       tag="${rest%%:*}"; args="${rest#*:}"; log="gpurun_out/${tag}.log"
       echo "== step $n: python $args"
       timeout -k 10 600 python -u $args > "$log" 2>&1
+      rc=$?; tail -6 "$log" ;;
+    run)
+      tag="${rest%%:*}"; args="${rest#*:}"; log="gpurun_out/${tag}.log"
+      echo "== step $n: $args"
+      timeout -k 10 120 $args > "$log" 2>&1
       rc=$?; tail -6 "$log" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

@@ -51,6 +51,17 @@ case "$1" in
        $J "test:tests" && $J "bench:r06_s15_default:--detail gpurun_out/r06_s15_default_detail.json" ;;
   s16) # the per-rank slice (C3s8) and the headline: kernel traces of the timed windows
        $J "prof:r06_s16_c3s8_prof:$S8" "prof:r06_s16_prof:$H --ar-probe 0" ;;
+  s17) # the interior point's per-iteration arrays parked in LDS, the predictor's terms without the zero
+       # shift / second-order terms, the KKT check from iteration 6: parity, then Iter0 A/B (PHX_IPM_NO_PARK)
+       IPMNP="PHX_LANE_DEFS=PHX_IPM_NO_PARK"
+       $J "test:tests/test_gpu_parity.py tests/test_trajectories.py tests/test_hydro.py" && \
+       $J "run:r06_s17_rcp_acc:scripts/micro/rcp_acc" && \
+       $J "bench:r06_s17_h1:$H --ar-probe 0" && env $IPMNP $J "bench:r06_s17_h1_np:$H --ar-probe 0" && \
+       $J "bench:r06_s17_h2:$H --ar-probe 0" && env $IPMNP $J "bench:r06_s17_h2_np:$H --ar-probe 0" && \
+       $J "bench:r06_s17_1m:$M" && env $IPMNP $J "bench:r06_s17_1m_np:$M" && \
+       $J "bench:r06_s17_c4:--configs C4,C3s8 --no-cpu-baseline --no-conv --ar-probe 0 --steps 10 --warmup 1" && \
+       env $IPMNP $J "bench:r06_s17_c4_np:--configs C4,C3s8 --no-cpu-baseline --no-conv --ar-probe 0 --steps 10 --warmup 1" && \
+       $J "prof:r06_s17_prof:$H --ar-probe 0" ;;
   final) # the round's evidence: the whole GPU suite, smoke, the driver's default command, kernel traces
        $J "test:tests" && $J "py:r06_final_smoke:scripts/run_smoke.py" "bench:r06_final_default:--detail gpurun_out/r06_final_default_detail.json" \
           "prof:r06_final_prof:$H --ar-probe 0" "prof:r06_final_c3s8_prof:$S8" "prof:r06_final_1m_prof:$M" \
