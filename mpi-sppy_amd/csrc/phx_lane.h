@@ -627,23 +627,42 @@ PHX_LD void ipm_opaque(double* x, double* zl, double* zu, double* rl, double* ru
 // live set (farmer: ~340 VGPRs) overflowed into AGPRs, one accvgpr move per
 // 32-bit half per use (≈1,000 moves against ≈2,300 FP64 operations per
 // iteration, offline ISA).  The values read back are the values stored, so
-// the arithmetic is unchanged.  On only when the block fits 40 KB (one
+// the arithmetic is unchanged.  Parked while the block fits 40 KB (one
 // wavefront per SIMD, four blocks per CU); PHX_IPM_NO_PARK keeps registers.
+// (A two-wave build with a 20 KB budget spills 644 B per lane: offline ISA.)
 #if (defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC_RTC__)) && !defined(PHX_IPM_NO_PARK)
 #define PHX_IPM_PARK_ON 1
 #else
 #define PHX_IPM_PARK_ON 0
 #endif
+#ifndef PHX_IPM_PARK_BYTES
+#define PHX_IPM_PARK_BYTES 40960
+#endif
 template <class PT>
 struct IpmPark {
     static constexpr int NN = PT::NMAX_N, MM = PT::NMAX_M, TT = PT::NMAX_M * (PT::NMAX_M + 1) / 2;
-    static constexpr int OM = 0, ODX = TT, OIS = TT + NN, ODXA = TT + NN + MM, ODSA = TT + 2 * NN + MM;
-    static constexpr int SIZE = TT + 2 * NN + 2 * MM;
-    static constexpr bool ON = PHX_IPM_PARK_ON && SIZE * 64 * 8 <= 40960;
+    // in priority order while the block's bytes fit PHX_IPM_PARK_BYTES (one
+    // wavefront per SIMD: 40 KB; two: 20 KB): M | Dx | isig | dxa | dsa | the
+    // reciprocal slacks rl ru rwl rwu (farmer: the first five at 40 KB, aircond
+    // the first three.  A 96 KB budget for batches of at most one block per CU,
+    // where every array fits, was measured slower: C4 Iter0 0.281 / 0.287 against
+    // 0.265 / 0.269 ms, C3s8 0.153 / 0.170 against 0.148 / 0.145, r06_s19)
+    static constexpr bool fits(int slots) { return PHX_IPM_PARK_ON && slots * 64 * 8 <= PHX_IPM_PARK_BYTES; }
+    static constexpr bool PM = fits(TT), PDX = PM && fits(TT + NN), PIS = PDX && fits(TT + NN + MM),
+                          PDXA = PIS && fits(TT + 2 * NN + MM), PDSA = PDXA && fits(TT + 2 * NN + 2 * MM),
+                          PR = PDSA && fits(TT + 4 * NN + 4 * MM);
+    static constexpr int OM = 0, ODX = TT, OIS = TT + NN, ODXA = TT + NN + MM, ODSA = TT + 2 * NN + MM,
+                         ORL = TT + 2 * NN + 2 * MM, ORU = ORL + NN, ORWL = ORU + NN, ORWU = ORWL + MM;
+    static constexpr int SIZE = PR ? TT + 4 * NN + 4 * MM : PDSA ? TT + 2 * NN + 2 * MM : PDXA ? TT + 2 * NN + MM
+                              : PIS ? TT + NN + MM : PDX ? TT + NN : PM ? TT : 0;
+    static constexpr bool ON = SIZE > 0;
+    static constexpr bool on(int off) {
+        return off == OM ? PM : off == ODX ? PDX : off == OIS ? PIS : off == ODXA ? PDXA : off == ODSA ? PDSA : PR;
+    }
 };
 template <class PT, int K>
 PHX_LD void ipm_put(double* lds, const double* v, int off) {
-    if (IpmPark<PT>::ON) {
+    if (IpmPark<PT>::on(off)) {
 #if PHX_IPM_PARK_ON
         const int l = threadIdx.x;
         PHX_UNROLL for (int k = 0; k < K; ++k) lds[(off + k) * 64 + l] = v[k];
@@ -652,12 +671,29 @@ PHX_LD void ipm_put(double* lds, const double* v, int off) {
 }
 template <class PT, int K>
 PHX_LD void ipm_get(const double* lds, double* v, int off) {
-    if (IpmPark<PT>::ON) {
+    if (IpmPark<PT>::on(off)) {
 #if PHX_IPM_PARK_ON
         const int l = opaque_index(threadIdx.x);
         PHX_UNROLL for (int k = 0; k < K; ++k) v[k] = lds[(off + k) * 64 + l];
 #endif
     }
+}
+// the reciprocal slacks, all four
+template <class PT>
+PHX_LD void ipm_put_r(double* lds, const double* rl, const double* ru, const double* rwl, const double* rwu) {
+    typedef IpmPark<PT> PK;
+    ipm_put<PT, PK::NN>(lds, rl, PK::ORL);
+    ipm_put<PT, PK::NN>(lds, ru, PK::ORU);
+    ipm_put<PT, PK::MM>(lds, rwl, PK::ORWL);
+    ipm_put<PT, PK::MM>(lds, rwu, PK::ORWU);
+}
+template <class PT>
+PHX_LD void ipm_get_r(const double* lds, double* rl, double* ru, double* rwl, double* rwu) {
+    typedef IpmPark<PT> PK;
+    ipm_get<PT, PK::NN>(lds, rl, PK::ORL);
+    ipm_get<PT, PK::NN>(lds, ru, PK::ORU);
+    ipm_get<PT, PK::MM>(lds, rwl, PK::ORWL);
+    ipm_get<PT, PK::MM>(lds, rwu, PK::ORWU);
 }
 
 #ifndef PHX_IPM_CHECK_FROM
@@ -775,12 +811,14 @@ PHX_LD double ipm_core(const Data<PT>& D, int max_it, double tol, double* x, dou
         ipm_put<PT, TT>(ipm_lds, M, PK::OM);
         ipm_put<PT, NN>(ipm_lds, Dx, PK::ODX);
         ipm_put<PT, MM>(ipm_lds, isig, PK::OIS);
+        ipm_put_r<PT>(ipm_lds, rl, ru, rwl, rwu);
         // predictor (pass 0, smu = 0) then corrector (pass 1)
         double smu = 0.0, ap = 1.0, ad = 1.0;
         double dx[NN], ds[MM], dy[MM], dxa[NN], dsa[MM];
         PHX_UNROLL for (int j = 0; j < PT::n(); ++j) dxa[j] = 0.0;
         PHX_UNROLL for (int i = 0; i < PT::m(); ++i) dsa[i] = 0.0;
         PHX_IPM_PASS_LOOP for (int pass = 0; pass < 2; ++pass) {
+            ipm_get_r<PT>(ipm_lds, rl, ru, rwl, rwu);
             ipm_opaque<PT>(x, zl, zu, rl, ru, s, wl, wu, rwl, rwu, y);
             if (pass == 1) ipm_get<PT, NN>(ipm_lds, dxa, PK::ODXA);
             ipm_get<PT, NN>(ipm_lds, Dx, PK::ODX);
@@ -832,6 +870,7 @@ PHX_LD double ipm_core(const Data<PT>& D, int max_it, double tol, double* x, dou
             ipm_get<PT, MM>(ipm_lds, isig, PK::OIS);
             PHX_UNROLL for (int i = 0; i < PT::m(); ++i)
                 ds[i] = (PT::eq(i) || row_free<PT>(i)) ? 0.0 : (ds[i] - dy[i]) * isig[i];
+            ipm_get_r<PT>(ipm_lds, rl, ru, rwl, rwu);
             ipm_opaque<PT>(x, zl, zu, rl, ru, s, wl, wu, rwl, rwu, y);
             // step lengths as inverse ratios (step = 1 / max(1, max ratio)),
             // multiplier steps recomputed from dx, ds
@@ -927,6 +966,7 @@ PHX_LD double ipm_core(const Data<PT>& D, int max_it, double tol, double* x, dou
         ad = fmin(1.0, 0.995 * ad);
         ipm_get<PT, NN>(ipm_lds, dxa, PK::ODXA);
         ipm_get<PT, MM>(ipm_lds, dsa, PK::ODSA);
+        ipm_get_r<PT>(ipm_lds, rl, ru, rwl, rwu);
         PHX_UNROLL for (int j = 0; j < PT::n(); ++j) {
             if (has_lo<PT>(j)) {
                 const double sl = x[j] - D.l(j);

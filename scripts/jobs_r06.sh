@@ -62,6 +62,23 @@ case "$1" in
        $J "bench:r06_s17_c4:--configs C4,C3s8 --no-cpu-baseline --no-conv --ar-probe 0 --steps 10 --warmup 1" && \
        env $IPMNP $J "bench:r06_s17_c4_np:--configs C4,C3s8 --no-cpu-baseline --no-conv --ar-probe 0 --steps 10 --warmup 1" && \
        $J "prof:r06_s17_prof:$H --ar-probe 0" ;;
+  s18) # the first PH iteration as a fused launch with the rescue round budget (PHX_FUSED_FIRST=1) against the
+       # unfused body (k_xbar + k_update_w_seg + warm pass + rescue list + gated cold pass): A/B, traces
+       FF="PHX_FUSED_FIRST=1"
+       $J "bench:r06_s18_h1:$H --ar-probe 0" && env $FF $J "bench:r06_s18_h1_ff:$H --ar-probe 0" && \
+       $J "bench:r06_s18_h2:$H --ar-probe 0" && env $FF $J "bench:r06_s18_h2_ff:$H --ar-probe 0" && \
+       $J "bench:r06_s18_1m:$M" && env $FF $J "bench:r06_s18_1m_ff:$M" && \
+       $J "bench:r06_s18_s8:--configs C3s8 --no-cpu-baseline --no-conv --ar-probe 0" && \
+       env $FF $J "bench:r06_s18_s8_ff:--configs C3s8 --no-cpu-baseline --no-conv --ar-probe 0" && \
+       env $FF $J "prof:r06_s18_prof_ff:$H --ar-probe 0" ;;
+  s19) # batches of at most one lane block per CU: the interior point parks all its per-iteration arrays (96 KB
+       # budget): parity, C4 / C3s8 A/B against the 40 KB budget
+       P40="PHX_LANE_DEFS=PHX_IPM_PARK_BYTES=40960"
+       Q="--configs C4,C3s8 --no-cpu-baseline --no-conv --ar-probe 0 --steps 10 --warmup 1"
+       $J "test:tests/test_gpu_parity.py tests/test_trajectories.py tests/test_hydro.py tests/test_distributed_gpu.py" && \
+       $J "bench:r06_s19_a1:$Q" && env $P40 $J "bench:r06_s19_a1_40:$Q" && \
+       $J "bench:r06_s19_a2:$Q" && env $P40 $J "bench:r06_s19_a2_40:$Q" && \
+       $J "prof:r06_s19_c4_prof:--only C4 $A" "prof:r06_s19_c3s8_prof:$S8" ;;
   final) # the round's evidence: the whole GPU suite, smoke, the driver's default command, kernel traces
        $J "test:tests" && $J "py:r06_final_smoke:scripts/run_smoke.py" "bench:r06_final_default:--detail gpurun_out/r06_final_default_detail.json" \
           "prof:r06_final_prof:$H --ar-probe 0" "prof:r06_final_c3s8_prof:$S8" "prof:r06_final_1m_prof:$M" \
