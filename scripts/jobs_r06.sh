@@ -79,6 +79,30 @@ case "$1" in
        $J "bench:r06_s19_a1:$Q" && env $P40 $J "bench:r06_s19_a1_40:$Q" && \
        $J "bench:r06_s19_a2:$Q" && env $P40 $J "bench:r06_s19_a2_40:$Q" && \
        $J "prof:r06_s19_c4_prof:--only C4 $A" "prof:r06_s19_c3s8_prof:$S8" ;;
+  s20) # C4: bounded multi-change rescue updates (PHX_MULTI_THETA, a JIT define) on the GPU, A/B against the
+       # single-change rounds, alternating on one box
+       Q="--configs C4 --no-cpu-baseline --no-conv --ar-probe 0 --steps 10 --warmup 1"
+       T2="PHX_LANE_DEFS=PHX_MULTI_THETA=0.2 PHX_MULTI_ROUNDS=4"
+       T5="PHX_LANE_DEFS=PHX_MULTI_THETA=0.5 PHX_MULTI_ROUNDS=4"
+       T8="PHX_LANE_DEFS=PHX_MULTI_THETA=0.2 PHX_MULTI_ROUNDS=8"
+       $J "bench:r06_s20_a:$Q" && env "$T2" $J "bench:r06_s20_t2:$Q" && env "$T5" $J "bench:r06_s20_t5:$Q" && \
+       env "$T8" $J "bench:r06_s20_t8:$Q" && $J "bench:r06_s20_b:$Q" && env "$T2" $J "bench:r06_s20_t2b:$Q" ;;
+  s21) # where the sparse solver's time goes: phase clocks (PHX_SP_PROF) of C5a's leftover pass and C5b
+       PHX_SP_PROF=1 $J "bench:r06_s21_c5a_spprof:--only C5a $A" && PHX_SP_PROF=1 $J "bench:r06_s21_c5b_spprof:--only C5b $A" ;;
+  s22) # bounded multi-change updates: the theta / rounds neighbourhood on C4, and their effect on farmer (the
+       # headline, C3s8, C1: the rescue pass of the first PH iteration); the sparse phase clocks; a C3s8 trace
+       Q="--configs C4 --no-cpu-baseline --no-conv --ar-probe 0 --steps 10 --warmup 1"
+       F="--configs C3s8,C1 --no-cpu-baseline --no-conv --ar-probe 0"
+       D="PHX_LANE_DEFS=PHX_MULTI_THETA=0.2 PHX_MULTI_ROUNDS=4"
+       env "PHX_LANE_DEFS=PHX_MULTI_THETA=0.1 PHX_MULTI_ROUNDS=4" $J "bench:r06_s22_t1r4:$Q" && \
+       env "PHX_LANE_DEFS=PHX_MULTI_THETA=0.3 PHX_MULTI_ROUNDS=4" $J "bench:r06_s22_t3r4:$Q" && \
+       env "PHX_LANE_DEFS=PHX_MULTI_THETA=0.2 PHX_MULTI_ROUNDS=2" $J "bench:r06_s22_t2r2:$Q" && \
+       env "PHX_LANE_DEFS=PHX_MULTI_THETA=0.2 PHX_MULTI_ROUNDS=6" $J "bench:r06_s22_t2r6:$Q" && \
+       env "PHX_LANE_DEFS=PHX_MULTI_THETA=0.2 PHX_MULTI_ROUNDS=3" $J "bench:r06_s22_t2r3:$Q" && \
+       $J "bench:r06_s22_f:$F" && env "$D" $J "bench:r06_s22_f_t2:$F" && \
+       $J "bench:r06_s22_f2:$F" && env "$D" $J "bench:r06_s22_f2_t2:$F" && \
+       PHX_SP_PROF=1 $J "bench:r06_s22_c5a_spprof:--only C5a $A" && PHX_SP_PROF=1 $J "bench:r06_s22_c5b_spprof:--only C5b $A" && \
+       $J "prof:r06_s22_c3s8_prof:$S8" ;;
   final) # the round's evidence: the whole GPU suite, smoke, the driver's default command, kernel traces
        $J "test:tests" && $J "py:r06_final_smoke:scripts/run_smoke.py" "bench:r06_final_default:--detail gpurun_out/r06_final_default_detail.json" \
           "prof:r06_final_prof:$H --ar-probe 0" "prof:r06_final_c3s8_prof:$S8" "prof:r06_final_1m_prof:$M" \
