@@ -337,6 +337,14 @@ def workloads():
                    # (r06 s9 trace), so they run in a second timed run of their own:
                    # the metric's run records none
                    kernel_timing={"iterk_timing": -1},
+                   # bounded multi-change active-set updates (every violation within
+                   # 0.2 of the worst, 4 rounds, then single changes): the early
+                   # iterations' rescue tails on 1-3 lanes set phx_lane_all's time --
+                   # steady step 0.121 / 0.121 -> 0.111 / 0.110 ms over two pairs on one
+                   # box (r06 s20); theta 0.1 / 0.3 and 2 / 3 / 6 rounds 0.114-0.122
+                   # (r06 s22).  On farmer the same setting costs 6 % (headline) to
+                   # 14 % (C3s8), so it is this problem's option, not a default
+                   so={"lane_multi_theta": 0.2, "lane_multi_rounds": 4},
                    cpu=dict(model="aircond", scens=1000, iters=40, total=1000)),
         "C5a": dict(creator=sslp.scenario_creator, names=lambda S: sslp.scenario_names_creator(10000),
                     kw=lambda S, cm: {"num_scens": 10000}, nodes=None, S=10000,

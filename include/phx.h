@@ -58,6 +58,14 @@ typedef struct phx_problem_desc {
     int32_t c_vary, bnd_vary, rhs_vary;
     const int32_t* slot_col;/* [N]  column of each nonant slot, in the
                                reference's nonant order (spbase.py:293-302)   */
+    /* Lane-solver tuning compiled into the structure-specialised kernels
+     * (phx_jit.h); zero-initialised means off.  lane_multi_theta > 0: the
+     * first lane_multi_rounds (0: 4) active-set rounds after the full
+     * primal-dual updates change every violation within lane_multi_theta of
+     * the worst one instead of the worst alone (phx_lane.h multi_violations;
+     * the engine's solver option of the same name, SPOpt).                   */
+    double  lane_multi_theta;
+    int32_t lane_multi_rounds;
 } phx_problem_desc;
 
 /* Solver knobs; the engine fills them from options["iter0_solver_options"] /

@@ -30,6 +30,7 @@ class ProblemDesc(ctypes.Structure):
         ("bl", c_void_p), ("bu", c_void_p),
         ("c_vary", c_int32), ("bnd_vary", c_int32), ("rhs_vary", c_int32),
         ("slot_col", c_void_p),
+        ("lane_multi_theta", ctypes.c_double), ("lane_multi_rounds", c_int32),
     ]
 
 

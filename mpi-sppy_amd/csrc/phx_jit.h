@@ -45,6 +45,10 @@ struct LaneStructure {
     // the interior point's start scales (lane_scales): primal offsets from the
     // bounds / row sides, bound and row multipliers
     double ipm_xs = 1.0, ipm_zs = 1.0, ipm_ws = 1.0;
+    // bounded multi-change active-set updates (phx_lane.h multi_violations):
+    // theta (0: off) for the first multi_rounds rounds after single_after
+    double multi_theta = 0.0;
+    int multi_rounds = 0;
 };
 
 // median of the nonzero finite magnitudes (0 if none)
@@ -77,6 +81,14 @@ inline void set_lane_values(LaneStructure& L, const std::vector<double>& Ac, con
     L.ub = L.bnd_vary ? std::vector<double>() : ub;
     L.bl = L.rhs_vary ? std::vector<double>() : bl;
     L.bu = L.rhs_vary ? std::vector<double>() : bu;
+}
+
+// The caller's lane-solver tuning (phx_problem_desc lane_multi_*): a theta
+// outside (0, 1] or not finite is off; rounds 0 means 4
+inline void set_lane_tuning(LaneStructure& L, double multi_theta, int multi_rounds) {
+    const bool on = std::isfinite(multi_theta) && multi_theta > 0.0 && multi_theta <= 1.0;
+    L.multi_theta = on ? multi_theta : 0.0;
+    L.multi_rounds = on ? (multi_rounds > 0 ? std::min(multi_rounds, 64) : 4) : 0;
 }
 
 // Limits for the register-resident kernel (beyond them: generic kernels).
@@ -219,12 +231,26 @@ inline std::string lane_kernel_source(const LaneStructure& L, int warm_waves = 1
     o << "  __host__ __device__ static constexpr bool rhs_vary() { return " << (L.rhs_vary ? "true" : "false")
       << "; }\n";
     {
-        char buf[160];
+        char buf[512];
         snprintf(buf, sizeof(buf), "  __host__ __device__ static constexpr double ipm_xs() { return %a; }\n", L.ipm_xs);
         o << buf;
         snprintf(buf, sizeof(buf), "  __host__ __device__ static constexpr double ipm_zs() { return %a; }\n", L.ipm_zs);
         o << buf;
         snprintf(buf, sizeof(buf), "  __host__ __device__ static constexpr double ipm_ws() { return %a; }\n", L.ipm_ws);
+        o << buf;
+        // the bounded multi-change update (phx_lane.h multi_violations); a
+        // PHX_MULTI_THETA / PHX_MULTI_ROUNDS define (PHX_LANE_DEFS) overrides
+        snprintf(buf, sizeof(buf),
+                 "#ifdef PHX_MULTI_THETA\n  __host__ __device__ static constexpr double multi_theta() { return "
+                 "PHX_MULTI_THETA; }\n#else\n  __host__ __device__ static constexpr double multi_theta() { return %a; "
+                 "}\n#endif\n",
+                 L.multi_theta);
+        o << buf;
+        snprintf(buf, sizeof(buf),
+                 "#ifdef PHX_MULTI_ROUNDS\n  __host__ __device__ static constexpr int multi_rounds() { return "
+                 "PHX_MULTI_ROUNDS; }\n#else\n  __host__ __device__ static constexpr int multi_rounds() { return %d; "
+                 "}\n#endif\n",
+                 L.multi_rounds);
         o << buf;
     }
     emit_table(o, "int", "row", L.row);

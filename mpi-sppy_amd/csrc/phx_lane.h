@@ -1508,10 +1508,14 @@ PHX_LD int worst_violation(const Data<PT>& D, CM enter_lo, CM enter_up, CM leave
 #endif
 }
 
-#ifdef PHX_MULTI_THETA
-// (experiment) the flagged changes whose relative violation is at least theta
-// times the largest one (worst_violation's measures): a bounded update between
-// the full primal-dual update and a single change
+// Bounded multi-change update: the flagged changes whose relative violation is
+// at least theta times the largest one (worst_violation's measures) -- between
+// the full primal-dual update and a single change.  Used for the first
+// PT::multi_rounds() rounds after single_after when the problem's lane
+// structure sets PT::multi_theta() > 0 (phx_jit.h LaneStructure; a constexpr 0
+// compiles it out).  Aircond 10x10x10 (C4): the early iterations' rescue rounds
+// of single changes on 1-3 lanes set phx_lane_all's time; with theta 0.2 for
+// 4 rounds the step went 0.121 -> 0.111 ms (r06 s20, two pairs on one box).
 template <class PT, class CM>
 PHX_LD void multi_violations(const Data<PT>& D, CM& enter_lo, CM& enter_up, CM& leave, uint32_t& act_lo,
                              uint32_t& act_up, uint32_t& drop, const double* xp, const double* z, double qmax,
@@ -1554,7 +1558,6 @@ PHX_LD void multi_violations(const Data<PT>& D, CM& enter_lo, CM& enter_up, CM& 
     }
     enter_lo = el; enter_up = eu; leave = lv; act_lo = al; act_up = au; drop = dr;
 }
-#endif
 
 // KKT certificate of (xp, z) for active set a (unscaled, relative kkt_tol);
 // on failure applies the primal-dual active-set update (violated bounds/rows
@@ -1629,14 +1632,9 @@ PHX_LD int certify_update(const Data<PT>& D, ASet<PT>& a, const double* xp, cons
     }
     if (!(fin == 0.0)) return 2;      // not certified, and no update can repair it
     const bool changed = (enter_lo | enter_up | leave) != 0 || (act_lo | act_up | drop) != 0;
-#ifdef PHX_MULTI_THETA
-    if (multi && changed) {
-        multi_violations<PT>(D, enter_lo, enter_up, leave, act_lo, act_up, drop, xp, z, qmax, PHX_MULTI_THETA);
-    } else
-#else
-    (void)multi;
-#endif
-    if (single && changed) {
+    if (PT::multi_theta() > 0.0 && multi && changed) {
+        multi_violations<PT>(D, enter_lo, enter_up, leave, act_lo, act_up, drop, xp, z, qmax, PT::multi_theta());
+    } else if (single && changed) {
         // (the rare path: the violations' sizes are recomputed here so the
         // common certificate carries none of this)
         const int code = worst_violation<PT>(D, enter_lo, enter_up, leave, act_lo, act_up, drop, xp, z, qmax);
@@ -1679,13 +1677,11 @@ template <class PT, bool CARRY = PHX_CARRY_DEF, bool LEAN = false>
 PHX_LD int as_round(const LaneIO& io, const Data<PT>& D, ASet<PT>& a, double* xp, double* z, int r) {
     PHX_LANE_STAT(0);
     if (!kkt_solve<PT, CARRY, LEAN>(D, a, xp, z)) return 3;
-#ifdef PHX_MULTI_THETA
-    // (experiment) the first PHX_MULTI_ROUNDS rounds after single_after: bounded updates
+    // the first PT::multi_rounds() rounds after single_after: bounded updates
+    // (when the structure sets them)
     return certify_update<PT>(D, a, xp, z, io.kkt_tol, r >= io.single_after,
-                              r >= io.single_after && r < io.single_after + PHX_MULTI_ROUNDS);
-#else
-    return certify_update<PT>(D, a, xp, z, io.kkt_tol, r >= io.single_after);
-#endif
+                              PT::multi_theta() > 0.0 && r >= io.single_after &&
+                                  r < io.single_after + PT::multi_rounds());
 }
 // r0: the index of the first round (the fused kernel runs round 0 itself)
 // (a certified lane is written by the caller from re-loaded data: writing it

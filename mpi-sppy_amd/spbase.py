@@ -401,6 +401,12 @@ class SPBase:
         for k in ["rowptr", "colidx", "kvar", "Aconst", "Avar", "c", "lb", "ub", "bl", "bu", "slot_col"]:
             setattr(desc, k, d[k].data_ptr())
         desc.c_vary, desc.bnd_vary, desc.rhs_vary = int(b.c_vary), int(b.bnd_vary), int(b.rhs_vary)
+        # lane-solver tuning compiled with the problem (solver options
+        # lane_multi_theta / lane_multi_rounds; iterk's over iter0's)
+        so = dict(self.options.get("iter0_solver_options") or {})
+        so.update(self.options.get("iterk_solver_options") or {})
+        desc.lane_multi_theta = float(so.get("lane_multi_theta", 0.0) or 0.0)
+        desc.lane_multi_rounds = int(so.get("lane_multi_rounds", 0) or 0)
         lib.check(self._ctx, lib.set_problem(self._ctx, desc), "set_problem")
         self._desc = desc
         # PH state

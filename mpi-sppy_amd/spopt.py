@@ -15,6 +15,12 @@ phbase.py:273-275): keys ``pdhg_max_iters``, ``pdhg_check_every``,
 ``kkt_tol``, ``opt_tol``, ``polish_reg``, ``warm_start``, ``ipm_after``,
 ``ipm_max_it``, ``ipm_tol``, ``lane_solver``, ``as_rounds``, ``warm_passes``, ``wg_warm``, ``wg_first``,
 ``sp``, ``sp_rounds``, ``seed_templates``, ``rescue_rounds``, ``lane_ipm_tol``.
+Two more are read once, when the problem is set up (``SPBase._upload_batch``),
+because they are compiled into the structure-specialised lane kernels:
+``lane_multi_theta`` (> 0: bounded multi-change active-set updates -- every
+violation within theta of the worst -- for ``lane_multi_rounds`` rounds, default
+4, after the full updates; 0: single changes, the default) and
+``lane_multi_rounds``.
 """
 import ctypes
 import inspect

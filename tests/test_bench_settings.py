@@ -9,6 +9,10 @@ which lanes stop the pipeline for the sparse solver).
 * C2: the full 1,000-scenario W / x-bar trajectory from the engine's Iter0
   point against the oracle's PH iterations (phbase.py:27-107, 293-343,
   875-979), as test_gpu_parity.test_farmer_cm10_1000_workgroup_gpu.
+* C4 (aircond 10x10x10) with bounded multi-change active-set updates
+  (lane_multi_theta 0.2, 4 rounds): test_engine_emu.check_aircond_multi_change
+  runs exactly this setting against the oracle (emulation 300 scenarios, GPU
+  the full 1,000).
 * C5a: the 256-scenario sslp trajectory against the oracle golden
   (tests/golden/traj_sslp_256.npz), as test_trajectories, and the full 10,000
   scenarios with sampled oracle re-solves, as test_sslp.test_sslp_10k_gpu."""
@@ -23,7 +27,8 @@ import bench
 
 def _bench_so(name):
     so = bench.workloads()[name]["so"]
-    assert so == {"C2": {"wg_warm": 8, "wg_first": 1}, "C5a": {"wg_warm": 4}}[name]   # the settings timed
+    assert so == {"C2": {"wg_warm": 8, "wg_first": 1}, "C5a": {"wg_warm": 4},
+                  "C4": {"lane_multi_theta": 0.2, "lane_multi_rounds": 4}}[name]   # the settings timed
     return dict(so)
 
 
@@ -84,3 +89,9 @@ def test_c5a_bench_settings_gpu(gpu_lib):
     o.solve_loop()
     assert rel(ph.nonant_values()[pick], o.xn()) < 1e-6
     assert rel(ph._host("obj")[pick], o.obj) < 1e-8
+
+
+def test_c4_bench_settings_are_the_tested_ones():
+    import test_engine_emu as te
+    so = _bench_so("C4")
+    assert (so["lane_multi_theta"], so["lane_multi_rounds"]) == te.MULTI_SETTING

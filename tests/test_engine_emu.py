@@ -70,6 +70,47 @@ def test_aircond_multistage_emu(emu):
     assert rel(xb["ROOT"][0], o.xbar[0, 0:2]) < 1e-12
 
 
+MULTI_SETTING = (0.2, 4)      # bench.py's C4 solver options (test_bench_settings pins them)
+
+
+def check_aircond_multi_change(lib, device, bfs, iters, tol_w):
+    """The bounded multi-change active-set updates (solver option
+    lane_multi_theta, compiled into the lane kernels): the same PH trajectory as
+    the oracle's (phbase.py:27-107, 293-343 via oracle/ph.py), and a different
+    round path than the single changes (the option is live)."""
+    names = ["scen%d" % i for i in range(int(np.prod(bfs)))]
+    nodes = sputils.create_nodenames_from_branching_factors(bfs)
+    runs = {}
+    for th in (0.0, MULTI_SETTING[0]):
+        so = {"lane_multi_theta": th, "lane_multi_rounds": MULTI_SETTING[1]}
+        runs[th] = run_engine(aircond.scenario_creator, names, {"branching_factors": bfs}, iters, lib=lib,
+                              device=device, all_nodenames=nodes,
+                              options={"iter0_solver_options": so, "iterk_solver_options": so})
+    ph, conv, Eobj, tb = runs[MULTI_SETTING[0]]
+    assert all_certified(ph)
+    o = oph.OraclePH([om.aircond(n, bfs) for n in names], rho=1.0)
+    oc, oE, otb = o.ph_main(iters)
+    assert rel(tb, otb) < 1e-9
+    assert rel(Eobj, oE) < 1e-8
+    assert rel(ph.W_array(), o.W) < tol_w
+    assert rel(conv, oc) < 1e-6
+    return runs
+
+
+def test_aircond_multi_change_emu(emu):
+    runs = check_aircond_multi_change(emu, "cpu", [10, 10, 3], 3, 1e-8)
+    assert not np.array_equal(runs[0.0][0]._host("x"), runs[MULTI_SETTING[0]][0]._host("x"))
+
+
+@pytest.mark.gpu
+def test_aircond_bf10x10x10_multi_change_gpu(gpu_lib):
+    """configs[3] with the bench's C4 setting (lane_multi_theta 0.2, 4 rounds)
+    through the device loop, vs the oracle (as test_aircond_bf10x10x10_gpu)."""
+    runs = check_aircond_multi_change(gpu_lib, None, [10, 10, 10], 3, 1e-6)
+    assert hasattr(runs[MULTI_SETTING[0]][0], "iterk_stats")
+    assert len(runs[MULTI_SETTING[0]][0].xbar_by_node()) == 111
+
+
 def test_docs_farmer_via_engine(emu):
     """doc/src/examples.rst trajectory (rho 10, 5 iterations) through the engine."""
     from mpisppy_amd import model as lm
