@@ -106,7 +106,7 @@ case "$1" in
   s23) # the multi-change setting as C4's solver option (lane_multi_theta, compiled with the problem): parity
        # tests, then the default configs path for C4 twice
        Q="--configs C4 --no-cpu-baseline --no-conv --ar-probe 0 --steps 10 --warmup 1"
-       $J "test:tests/test_engine_emu.py tests/test_bench_settings.py tests/test_gpu_parity.py -k aircond or bench_settings or multi" && \
+       $J "test:tests/test_engine_emu.py tests/test_bench_settings.py tests/test_gpu_parity.py::test_aircond_bf10x10x10_gpu" && \
        $J "bench:r06_s23_c4:$Q" && $J "bench:r06_s23_c4b:$Q" ;;
   final) # the round's evidence: the whole GPU suite, smoke, the driver's default command, kernel traces
        $J "test:tests" && $J "py:r06_final_smoke:scripts/run_smoke.py" "bench:r06_final_default:--detail gpurun_out/r06_final_default_detail.json" \
