@@ -43,6 +43,7 @@ Inputs resident in HBM before timing.  Extra keys:
                 projected)
 """
 import argparse
+import gc
 import json
 import os
 import subprocess
@@ -377,6 +378,33 @@ def timed_run(ph, K, dev):
     ph.PH_Prep()
     ph.subproblem_creation(False)
     ph.options["PHIterLimit"] = K
+    # Python's cyclic garbage collector off inside the timed region (as timeit
+    # does), after a full collection outside it: a generation-2 collection over
+    # the process's ~10^6 objects (torch's among them) stalls the host for
+    # ~10-15 ms, and the GPU idles behind it -- seen as 7-14e7 instead of ~1.9e9
+    # on runs where the allocation counters happened to trigger one inside the
+    # region (r06 s23 / s24).  No work of the path is skipped: the collector
+    # frees nothing the path allocates
+    with no_gc():
+        return _timed_region(ph, dev)
+
+
+class no_gc:
+    """A full collection, then the cyclic collector off until exit (timed regions)."""
+
+    def __enter__(self):
+        gc.collect()
+        self.was = gc.isenabled()
+        gc.disable()
+        return self
+
+    def __exit__(self, *exc):
+        if self.was:
+            gc.enable()
+        return False
+
+
+def _timed_region(ph, dev):
     ph.mpicomm.Barrier()
     dev.sync()
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)] if dev.cuda else None
@@ -701,11 +729,12 @@ def main():
     if not args.no_conv:
         ph2 = make_ph(hl, S, cm, args.rho, so, args.conv_max_iters, dev, convthresh=1e-4)
         dev.sync()
-        ph2.mpicomm.Barrier()
-        t0 = time.perf_counter()
-        ph2.ph_main(finalize=False)
-        dev.sync()
-        tc = dev.tensor([time.perf_counter() - t0])
+        with no_gc():                       # (as the timed run)
+            ph2.mpicomm.Barrier()
+            t0 = time.perf_counter()
+            ph2.ph_main(finalize=False)
+            dev.sync()
+            tc = dev.tensor([time.perf_counter() - t0])
         ph2.mpicomm.allreduce_max_(tc)
         res["conv_time"] = {"seconds": float(tc.item()), "iterations": ph2._PHIter, "conv": ph2.conv,
                             "convthresh": 1e-4, "converged": bool(ph2.conv is not None and ph2.conv < 1e-4)}
