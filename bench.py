@@ -379,23 +379,33 @@ def timed_run(ph, K, dev):
     ph.subproblem_creation(False)
     ph.options["PHIterLimit"] = K
     # Python's cyclic garbage collector off inside the timed region (as timeit
-    # does), after a full collection outside it: a generation-2 collection over
-    # the process's ~10^6 objects (torch's among them) stalls the host for
-    # ~10-15 ms, and the GPU idles behind it -- seen as 7-14e7 instead of ~1.9e9
-    # on runs where the allocation counters happened to trigger one inside the
-    # region (r06 s23 / s24).  No work of the path is skipped: the collector
-    # frees nothing the path allocates
+    # does): a generation-2 collection over the process's objects (torch's among
+    # them) stalled the host ~13 ms inside the region on some runs -- 7-14e7
+    # instead of ~1.9e9 (r06 s23 / s24) -- with the GPU idle behind it.  The
+    # full collection itself runs before the warm-up (gc_settle), not here: its
+    # walk over every object leaves the host's caches cold for the region.  No
+    # work of the path is skipped: the collector frees nothing the path allocates
     with no_gc():
         return _timed_region(ph, dev)
 
 
+def gc_settle():
+    """A full collection, then every surviving object frozen (gc.freeze: later
+    collections skip them) -- before a warm-up, outside any timed region."""
+    if os.environ.get("PHX_BENCH_GC") == "1":
+        return
+    gc.collect()
+    gc.freeze()
+
+
 class no_gc:
-    """A full collection, then the cyclic collector off until exit (timed regions)."""
+    """The cyclic collector off until exit (timed regions).  PHX_BENCH_GC=1 leaves
+    it on (A/B runs)."""
 
     def __enter__(self):
-        gc.collect()
         self.was = gc.isenabled()
-        gc.disable()
+        if os.environ.get("PHX_BENCH_GC") != "1":
+            gc.disable()
         return self
 
     def __exit__(self, *exc):
@@ -573,6 +583,7 @@ def run_config(name, w, args, K, so, world, dev):
     # object (each kernel's first launch -- code object load, the queue's
     # scratch growth -- outside the timed run)
     if args.warmup > 0:
+        gc_settle()
         ph = make_ph(w, S, 1, args.rho, so, args.warmup, dev)
         ph.ph_main(finalize=False)
         dev.sync()
@@ -663,6 +674,7 @@ def main():
     # before the timed region (the GPU does not idle between them while the
     # timed object is built) ----
     t = time.perf_counter()
+    gc_settle()
     ph = make_ph(hl, S, cm, args.rho, so, args.warmup, dev)
     print("[bench] warmup object built (%.1f s)" % (time.perf_counter() - t), file=sys.stderr, flush=True)
     ph.ph_main(finalize=False)

@@ -108,6 +108,12 @@ case "$1" in
        Q="--configs C4 --no-cpu-baseline --no-conv --ar-probe 0 --steps 10 --warmup 1"
        $J "test:tests/test_engine_emu.py tests/test_bench_settings.py tests/test_gpu_parity.py::test_aircond_bf10x10x10_gpu" && \
        $J "bench:r06_s23_c4:$Q" && $J "bench:r06_s23_c4b:$Q" ;;
+  s26) # the bench's collector handling (a full collection + freeze before each warm-up, the collector off in
+       # the timed regions) against the collector left on (PHX_BENCH_GC=1), alternating on one box
+       H2="--configs C4 --no-cpu-baseline --no-conv --ar-probe 0"
+       $J "bench:r06_s26_a1:$H2" && PHX_BENCH_GC=1 $J "bench:r06_s26_g1:$H2" && \
+       $J "bench:r06_s26_a2:$H2" && PHX_BENCH_GC=1 $J "bench:r06_s26_g2:$H2" && \
+       $J "bench:r06_s26_a3:$H2" && PHX_BENCH_GC=1 $J "bench:r06_s26_g3:$H2" ;;
   final) # the round's evidence: the whole GPU suite, smoke, the driver's default command, kernel traces
        $J "test:tests" && $J "py:r06_final_smoke:scripts/run_smoke.py" "bench:r06_final_default:--detail gpurun_out/r06_final_default_detail.json" \
           "prof:r06_final_prof:$H --ar-probe 0" "prof:r06_final_c3s8_prof:$S8" "prof:r06_final_1m_prof:$M" \
