@@ -114,6 +114,10 @@ case "$1" in
        $J "bench:r06_s26_a1:$H2" && PHX_BENCH_GC=1 $J "bench:r06_s26_g1:$H2" && \
        $J "bench:r06_s26_a2:$H2" && PHX_BENCH_GC=1 $J "bench:r06_s26_g2:$H2" && \
        $J "bench:r06_s26_a3:$H2" && PHX_BENCH_GC=1 $J "bench:r06_s26_g3:$H2" ;;
+  s27) # host time inside the timed region after the collector change (host_marks), C4's kernel trace with the
+       # multi-change setting, the headline's kernel + HIP runtime trace
+       $J "py:r06_s27_marks:scripts/host_marks.py 100000 20 5" "prof:r06_s27_c4_prof:--only C4 $A" \
+          "trace:r06_s27_trace:$H --ar-probe 0" ;;
   final) # the round's evidence: the whole GPU suite, smoke, the driver's default command, kernel traces
        $J "test:tests" && $J "py:r06_final_smoke:scripts/run_smoke.py" "bench:r06_final_default:--detail gpurun_out/r06_final_default_detail.json" \
           "prof:r06_final_prof:$H --ar-probe 0" "prof:r06_final_c3s8_prof:$S8" "prof:r06_final_1m_prof:$M" \
