@@ -74,6 +74,8 @@ def parse():
     ap.add_argument("--lane-solver", type=int, default=1, help="1: structure-specialised lane solver first")
     ap.add_argument("--depth", type=int, default=4, help="phx_iterk: iterations kept enqueued ahead")
     ap.add_argument("--fused", type=int, default=1, help="phx_iterk: one launch per PH iteration")
+    ap.add_argument("--kernel-timing-inline", action="store_true",
+                    help="record the kernel-timing events in the metric's own timed run (round-5 form)")
     ap.add_argument("--timing-every", type=int, default=-5,
                     help="phx_iterk: T > 0: HIP events around the lane kernel of every T-th iteration; "
                          "T < 0: fused loop: one event pair around all its launches (back to back: no "
@@ -662,10 +664,17 @@ def main():
         so.update(json.loads(args.so))
     S = args.scens if args.only is None else hl["S"]
     cm = args.cm if args.only is None else 1
+    # the metric's run records no events in its loop: the dominant kernel's
+    # launches are timed by phx_iterk's events in a second timed run of their own
+    # (same data, same K) -- each event record costs the stream ~6 us (r06 s27
+    # trace: the window's two records, 6.5 + 6.1 us of idle stream inside T);
+    # --kernel-timing-inline: the round-5 form, events in the metric's run
+    ktim = args.timing_every != 0 and not args.kernel_timing_inline
+    so_metric = dict(so, iterk_timing=0) if ktim else so
     # ---- the timed run's object (setup: outside the timed region) ----
     def build_timed():
         t = time.perf_counter()
-        obj = make_ph(hl, S, cm, args.rho, so, K, dev)
+        obj = make_ph(hl, S, cm, args.rho, so_metric, K, dev)
         dev.sync()
         return obj, time.perf_counter() - t
     if not args.build_after_warmup:
@@ -692,7 +701,14 @@ def main():
     st = getattr(ph, "iterk_stats", None)
     if st is not None and (st["iters"] != K or st["solves"] != K):
         raise RuntimeError("timed iterk_loop did not run %d full iterations: %s" % (K, st))
-    kernel, avg_s, launches, bpu, units = dominant_kernel(ph, K, args.fused)
+    if ktim:
+        phk = make_ph(hl, S, cm, args.rho, so, K, dev)
+        dev.sync()
+        timed_run(phk, K, dev)
+        kernel, avg_s, launches, bpu, units = dominant_kernel(phk, K, args.fused)
+        del phk
+    else:
+        kernel, avg_s, launches, bpu, units = dominant_kernel(ph, K, args.fused)
     b = ph.batch
     if world != 1:
         traffic, tsrc, tstat = None, None, "N > 1: per-rank PMC not collected"
@@ -739,7 +755,7 @@ def main():
     dev.empty_cache()
     # ---- time to conv < 1e-4 from Iter0 (fresh object, same data) ----
     if not args.no_conv:
-        ph2 = make_ph(hl, S, cm, args.rho, so, args.conv_max_iters, dev, convthresh=1e-4)
+        ph2 = make_ph(hl, S, cm, args.rho, so_metric, args.conv_max_iters, dev, convthresh=1e-4)
         dev.sync()
         with no_gc():                       # (as the timed run)
             ph2.mpicomm.Barrier()

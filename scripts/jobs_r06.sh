@@ -118,6 +118,12 @@ case "$1" in
        # multi-change setting, the headline's kernel + HIP runtime trace
        $J "py:r06_s27_marks:scripts/host_marks.py 100000 20 5" "prof:r06_s27_c4_prof:--only C4 $A" \
           "trace:r06_s27_trace:$H --ar-probe 0" ;;
+  s29) # the headline's kernel-timing events in a second timed run (the metric's run records none) against
+       # the round-5 form (--kernel-timing-inline), alternating on one box
+       $J "bench:r06_s29_a1:$H --ar-probe 0" && $J "bench:r06_s29_i1:$H --ar-probe 0 --kernel-timing-inline" && \
+       $J "bench:r06_s29_a2:$H --ar-probe 0" && $J "bench:r06_s29_i2:$H --ar-probe 0 --kernel-timing-inline" && \
+       $J "bench:r06_s29_a3:$H --ar-probe 0" && $J "bench:r06_s29_i3:$H --ar-probe 0 --kernel-timing-inline" && \
+       $J "bench:r06_s29_m:$M" ;;
   final) # the round's evidence: the whole GPU suite, smoke, the driver's default command, kernel traces
        $J "test:tests" && $J "py:r06_final_smoke:scripts/run_smoke.py" "bench:r06_final_default:--detail gpurun_out/r06_final_default_detail.json" \
           "prof:r06_final_prof:$H --ar-probe 0" "prof:r06_final_c3s8_prof:$S8" "prof:r06_final_1m_prof:$M" \
