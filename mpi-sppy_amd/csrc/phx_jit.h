@@ -382,6 +382,27 @@ inline std::string lane_kernel_source(const LaneStructure& L, int warm_waves = 1
          "    phx_lane::compact_lane(still, sc, io.lanes_out, io.count_out);\n"
          "  }\n"
          "}\n";
+    // the rescue list and the interior point of what it leaves, in one launch
+    // (phx_lane_warm_list, then phx_lane_cold + phx_lane_cold_as over its
+    // leftovers: the same per-lane functions and options, in that order)
+    o << "extern \"C\" __global__ void __launch_bounds__(64, 1) phx_lane_list_all(phx_lane::LaneIO io, "
+         "const int* lanes, const int* count, int as_cold) {\n"
+         "  if (phx_lane::gated(io.gate)) return;\n"
+         "  const int nl = *count;\n"
+         "  for (int base = blockIdx.x * 64; base < nl; base += gridDim.x * 64) {\n"
+         "    const int t = base + threadIdx.x;\n"
+         "    bool still = false;\n"
+         "    int sc = -1;\n"
+         "    if (t < nl) { sc = lanes[t]; still = " + wlr + "(io, sc); }\n"
+         "    if (still) {\n"
+         "      phx_lane::LaneIO io3 = io;\n"
+         "      io3.as_rounds = as_cold;\n"
+         "      phx_lane::ipm_lane<PT>(io3, sc);\n"
+         "      still = phx_lane::cold_rounds_lane<PT>(io3, sc);\n"
+         "    }\n"
+         "    phx_lane::compact_lane(still, sc, io.lanes_out, io.count_out);\n"
+         "  }\n"
+         "}\n";
     // Iter0 seeding: every lane takes the active set of its nearest certified
     // template (phx_lane.h seed_block: the template table staged in LDS)
     o << "extern \"C\" __global__ void __launch_bounds__(64) phx_lane_seed(phx_lane::LaneIO io, "

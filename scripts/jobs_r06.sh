@@ -124,6 +124,14 @@ case "$1" in
        $J "bench:r06_s29_a2:$H --ar-probe 0" && $J "bench:r06_s29_i2:$H --ar-probe 0 --kernel-timing-inline" && \
        $J "bench:r06_s29_a3:$H --ar-probe 0" && $J "bench:r06_s29_i3:$H --ar-probe 0 --kernel-timing-inline" && \
        $J "bench:r06_s29_m:$M" ;;
+  s30) # the rescue list and its cold pass in one launch (phx_lane_list_all) against the three launches
+       # (PHX_LIST_ALL=0): parity, then the headline and 1M alternating on one box, and a kernel trace
+       $J "test:tests/test_gpu_parity.py tests/test_trajectories.py tests/test_hydro.py tests/test_distributed_gpu.py tests/test_engine_emu.py" && \
+       $J "bench:r06_s30_a1:$H --ar-probe 0" && PHX_LIST_ALL=0 $J "bench:r06_s30_o1:$H --ar-probe 0" && \
+       $J "bench:r06_s30_a2:$H --ar-probe 0" && PHX_LIST_ALL=0 $J "bench:r06_s30_o2:$H --ar-probe 0" && \
+       $J "bench:r06_s30_a3:$H --ar-probe 0" && PHX_LIST_ALL=0 $J "bench:r06_s30_o3:$H --ar-probe 0" && \
+       $J "bench:r06_s30_m:$M" && PHX_LIST_ALL=0 $J "bench:r06_s30_mo:$M" && \
+       $J "prof:r06_s30_prof:$H --ar-probe 0" ;;
   final) # the round's evidence: the whole GPU suite, smoke, the driver's default command, kernel traces
        $J "test:tests" && $J "py:r06_final_smoke:scripts/run_smoke.py" "bench:r06_final_default:--detail gpurun_out/r06_final_default_detail.json" \
           "prof:r06_final_prof:$H --ar-probe 0" "prof:r06_final_c3s8_prof:$S8" "prof:r06_final_1m_prof:$M" \
