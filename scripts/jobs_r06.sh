@@ -132,6 +132,11 @@ case "$1" in
        $J "bench:r06_s30_a3:$H --ar-probe 0" && PHX_LIST_ALL=0 $J "bench:r06_s30_o3:$H --ar-probe 0" && \
        $J "bench:r06_s30_m:$M" && PHX_LIST_ALL=0 $J "bench:r06_s30_mo:$M" && \
        $J "prof:r06_s30_prof:$H --ar-probe 0" ;;
+  s31) # k_small_xw with every load at entry (slot columns by value, the node table and the ranks' counts
+       # prefetched before the gate): parity, C4 twice, C4 kernel trace
+       Q="--configs C4 --no-cpu-baseline --no-conv --ar-probe 0 --steps 10 --warmup 1"
+       $J "test:tests/test_gpu_parity.py tests/test_trajectories.py tests/test_hydro.py tests/test_engine_emu.py tests/test_bench_settings.py" && \
+       $J "bench:r06_s31_c4:$Q" && $J "bench:r06_s31_c4b:$Q" && $J "prof:r06_s31_c4_prof:--only C4 $A" ;;
   final) # the round's evidence: the whole GPU suite, smoke, the driver's default command, kernel traces
        $J "test:tests" && $J "py:r06_final_smoke:scripts/run_smoke.py" "bench:r06_final_default:--detail gpurun_out/r06_final_default_detail.json" \
           "prof:r06_final_prof:$H --ar-probe 0" "prof:r06_final_c3s8_prof:$S8" "prof:r06_final_1m_prof:$M" \
