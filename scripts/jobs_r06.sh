@@ -137,6 +137,18 @@ case "$1" in
        Q="--configs C4 --no-cpu-baseline --no-conv --ar-probe 0 --steps 10 --warmup 1"
        $J "test:tests/test_gpu_parity.py tests/test_trajectories.py tests/test_hydro.py tests/test_engine_emu.py tests/test_bench_settings.py" && \
        $J "bench:r06_s31_c4:$Q" && $J "bench:r06_s31_c4b:$Q" && $J "prof:r06_s31_c4_prof:--only C4 $A" ;;
+  s33) # the hybrid first iteration with its first pass fused (k_xbar + one fused launch + the rescue list +
+       # the decision kernel) against the unfused body (PHX_HYBRID_FUSED=0): the whole suite, then A/B
+       # alternating on one box (headline, C3s8, 1M)
+       HF="PHX_HYBRID_FUSED=0"
+       $J "test:tests" && \
+       $J "bench:r06_s33_a1:$H --ar-probe 0" && env $HF $J "bench:r06_s33_o1:$H --ar-probe 0" && \
+       $J "bench:r06_s33_a2:$H --ar-probe 0" && env $HF $J "bench:r06_s33_o2:$H --ar-probe 0" && \
+       $J "bench:r06_s33_a3:$H --ar-probe 0" && env $HF $J "bench:r06_s33_o3:$H --ar-probe 0" && \
+       $J "bench:r06_s33_s8:--configs C3s8 --no-cpu-baseline --no-conv --ar-probe 0" && \
+       env $HF $J "bench:r06_s33_s8o:--configs C3s8 --no-cpu-baseline --no-conv --ar-probe 0" && \
+       $J "bench:r06_s33_m:$M" && env $HF $J "bench:r06_s33_mo:$M" && \
+       $J "prof:r06_s33_prof:$H --ar-probe 0" ;;
   final) # the round's evidence: the whole GPU suite, smoke, the driver's default command, kernel traces
        $J "test:tests" && $J "py:r06_final_smoke:scripts/run_smoke.py" "bench:r06_final_default:--detail gpurun_out/r06_final_default_detail.json" \
           "prof:r06_final_prof:$H --ar-probe 0" "prof:r06_final_c3s8_prof:$S8" "prof:r06_final_1m_prof:$M" \
