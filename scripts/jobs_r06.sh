@@ -149,6 +149,12 @@ case "$1" in
        env $HF $J "bench:r06_s33_s8o:--configs C3s8 --no-cpu-baseline --no-conv --ar-probe 0" && \
        $J "bench:r06_s33_m:$M" && env $HF $J "bench:r06_s33_mo:$M" && \
        $J "prof:r06_s33_prof:$H --ar-probe 0" ;;
+  s34) # C4's lane-solver round budgets with the multi-change setting: as_rounds / rescue_rounds sweep
+       Q="--configs C4 --no-cpu-baseline --no-conv --ar-probe 0 --steps 10 --warmup 1"
+       $J "bench:r06_s34_d:$Q" && \
+       $J "bench:r06_s34_a3:$Q --so {\"as_rounds\":3}" && $J "bench:r06_s34_a6:$Q --so {\"as_rounds\":6}" && \
+       $J "bench:r06_s34_a8:$Q --so {\"as_rounds\":8}" && $J "bench:r06_s34_r16:$Q --so {\"rescue_rounds\":16}" && \
+       $J "bench:r06_s34_r64:$Q --so {\"rescue_rounds\":64}" && $J "bench:r06_s34_d2:$Q" ;;
   final) # the round's evidence: the whole GPU suite, smoke, the driver's default command, kernel traces
        $J "test:tests" && $J "py:r06_final_smoke:scripts/run_smoke.py" "bench:r06_final_default:--detail gpurun_out/r06_final_default_detail.json" \
           "prof:r06_final_prof:$H --ar-probe 0" "prof:r06_final_c3s8_prof:$S8" "prof:r06_final_1m_prof:$M" \
