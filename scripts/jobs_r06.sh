@@ -155,6 +155,11 @@ case "$1" in
        $J "bench:r06_s34_a3:$Q --so {\"as_rounds\":3}" && $J "bench:r06_s34_a6:$Q --so {\"as_rounds\":6}" && \
        $J "bench:r06_s34_a8:$Q --so {\"as_rounds\":8}" && $J "bench:r06_s34_r16:$Q --so {\"rescue_rounds\":16}" && \
        $J "bench:r06_s34_r64:$Q --so {\"rescue_rounds\":64}" && $J "bench:r06_s34_d2:$Q" ;;
+  s37) # C4: the warm passes' full-update rounds (single_after 3 by default) with the multi-change setting
+       Q="--configs C4 --no-cpu-baseline --no-conv --ar-probe 0 --steps 10 --warmup 1"
+       $J "bench:r06_s37_d:$Q" && PHX_WARM_SINGLE_AFTER=1 $J "bench:r06_s37_w1:$Q" && \
+       PHX_WARM_SINGLE_AFTER=2 $J "bench:r06_s37_w2:$Q" && PHX_WARM_SINGLE_AFTER=4 $J "bench:r06_s37_w4:$Q" && \
+       $J "bench:r06_s37_d2:$Q" && PHX_WARM_SINGLE_AFTER=2 $J "bench:r06_s37_w2b:$Q" ;;
   final) # the round's evidence: the whole GPU suite, smoke, the driver's default command, kernel traces
        $J "test:tests" && $J "py:r06_final_smoke:scripts/run_smoke.py" "bench:r06_final_default:--detail gpurun_out/r06_final_default_detail.json" \
           "prof:r06_final_prof:$H --ar-probe 0" "prof:r06_final_c3s8_prof:$S8" "prof:r06_final_1m_prof:$M" \
