@@ -740,7 +740,9 @@ def main():
         "steady": {"value": S * K / Tk, "ms_per_step": Tk * 1e3 / K, "def": "S K / T_iterk (Iter0 excluded)"},
         "roofline": dict(roofline(kernel, avg_s, launches, bpu, units, traffic, tsrc, tstat),
                          valu=valu_issue(kernel, "farmer100k", units, avg_s, simds=simds())
-                         if (world == 1 and args.only is None and S == 100000 and cm == 1) else None),
+                         if (world == 1 and args.only is None and S == 100000 and cm == 1) else None,
+                         timing_run=("a second timed run of the same K (the metric's run records no events)"
+                                     if ktim else "the metric's run")),
         "loop": ("PHBase.iterk_loop -> phx_iterk (device-driven, depth %d%s)"
                  % (args.depth, ", fused" if st and st.get("fused") else "")) if st else "PHBase host loop",
         "not_optimal": nbad, "setup_s": t_setup, "warmup_s": t_warm,
@@ -825,6 +827,8 @@ def _roof_short(rf, full=True):
         out["traffic_source"] = rf.get("traffic_source")
         st = rf.get("traffic_status") or ""
         out["traffic_current"] = st.startswith("current")
+        if rf.get("timing_run"):
+            out["timing_run"] = rf["timing_run"]
         v = rf.get("valu")
         if isinstance(v, dict) and not v.get("stale"):
             out["valu"] = {k: _r(v.get(k)) for k in ("valu_insts_per_wave", "waves_per_launch", "busiest_simd_waves",
