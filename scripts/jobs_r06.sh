@@ -160,6 +160,12 @@ case "$1" in
        $J "bench:r06_s37_d:$Q" && PHX_WARM_SINGLE_AFTER=1 $J "bench:r06_s37_w1:$Q" && \
        PHX_WARM_SINGLE_AFTER=2 $J "bench:r06_s37_w2:$Q" && PHX_WARM_SINGLE_AFTER=4 $J "bench:r06_s37_w4:$Q" && \
        $J "bench:r06_s37_d2:$Q" && PHX_WARM_SINGLE_AFTER=2 $J "bench:r06_s37_w2b:$Q" ;;
+  s38) # C4 / C3s8: phx_lane_all re-loading its data per round (PHX_ALL_RELOAD, a JIT define: fewer registers,
+       # aircond's 740 B/lane spill) against the register build, alternating
+       Q="--configs C4,C3s8 --no-cpu-baseline --no-conv --ar-probe 0 --steps 10 --warmup 1"
+       R="PHX_LANE_DEFS=PHX_ALL_RELOAD"
+       $J "bench:r06_s38_a:$Q" && env $R $J "bench:r06_s38_r:$Q" && \
+       $J "bench:r06_s38_a2:$Q" && env $R $J "bench:r06_s38_r2:$Q" ;;
   final) # the round's evidence: the whole GPU suite, smoke, the driver's default command, kernel traces
        $J "test:tests" && $J "py:r06_final_smoke:scripts/run_smoke.py" "bench:r06_final_default:--detail gpurun_out/r06_final_default_detail.json" \
           "prof:r06_final_prof:$H --ar-probe 0" "prof:r06_final_c3s8_prof:$S8" "prof:r06_final_1m_prof:$M" \
