@@ -523,6 +523,9 @@ def dominant_kernel(ph, K, fused):
                     kname = "phx_lane_warm_fzc"
             else:
                 kname = "phx_lane_all" if small else "phx_lane_warm"
+                # (the build that re-loads per round where the register build spills)
+                if small and "all=reload" in info:
+                    kname = "phx_lane_all_rl"
             return (kname, st["lane_warm_ms"] / 1e3 / st["warm_launches"], st["warm_launches"],
                     lane_bytes(b, fused=bool(st.get("fused")) and fused), b.S)
         if "workgroup solver on" in info:

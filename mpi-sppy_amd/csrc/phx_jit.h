@@ -347,6 +347,16 @@ inline std::string lane_kernel_source(const LaneStructure& L, int warm_waves = 1
          "  if (t < io.S) still = phx_lane::all_lane<PT>(io, t, rescue);\n"
          "  phx_lane::compact_lane(still, t, io.lanes_out, io.count_out);\n"
          "}\n";
+    // ... its build that re-loads the lane's data per round (the host uses it
+    // when phx_lane_all spills to scratch)
+    o << "extern \"C\" __global__ void __launch_bounds__(64, 1) phx_lane_all_rl(phx_lane::LaneIO io, int rescue) {\n"
+         "  if (phx_lane::gated(io.gate)) return;\n"
+         "  phx_lane::zero_next_counts(io.counts_next);\n"
+         "  const int t = blockIdx.x * 64 + threadIdx.x;\n"
+         "  bool still = false;\n"
+         "  if (t < io.S) still = phx_lane::all_lane<PT, false>(io, t, rescue);\n"
+         "  phx_lane::compact_lane(still, t, io.lanes_out, io.count_out);\n"
+         "}\n";
     // phx_iterk fused mode, after the last enqueued iteration: the decision on
     // its conv (the next warm launch's prologue does it otherwise)
     // (and the copies the host reads after the drain, whether or not the loop

@@ -1987,14 +1987,16 @@ PHX_LD bool cold_rounds_lane(const LaneIO& io, int sc) {
 // in the same order as the warm, rescue-list and cold passes, so the same
 // results, in one launch instead of four (three of them usually empty).
 // true: the lane needs the generic path.
-template <class PT>
-PHX_LD bool all_lane(const LaneIO& io, int sc, int rescue) {
-    // (the rounds on the data loaded at entry; PHX_ALL_RELOAD: re-loaded per round)
+// REG: the rounds on the data loaded at entry (phx_lane_all); false: re-loaded
+// per round (phx_lane_all_rl, which the host picks when the register build
+// spills -- aircond: 740 B/lane of scratch; PHX_ALL_RELOAD forces it)
 #ifdef PHX_ALL_RELOAD
-    constexpr bool REG = false;
+#define PHX_ALL_REG_DEF false
 #else
-    constexpr bool REG = true;
+#define PHX_ALL_REG_DEF true
 #endif
+template <class PT, bool REG = PHX_ALL_REG_DEF>
+PHX_LD bool all_lane(const LaneIO& io, int sc, int rescue) {
     if (!warm_lane<PT, false, REG>(io, sc)) return false;
     if (rescue > 0) {
         LaneIO io2 = io;

@@ -166,6 +166,11 @@ case "$1" in
        R="PHX_LANE_DEFS=PHX_ALL_RELOAD"
        $J "bench:r06_s38_a:$Q" && env $R $J "bench:r06_s38_r:$Q" && \
        $J "bench:r06_s38_a2:$Q" && env $R $J "bench:r06_s38_r2:$Q" ;;
+  s39) # phx_lane_all's re-loading build where the register build spills (aircond) + k_small_xw's scans
+       # without key shuffles: parity, C4 / C3s8 twice, C4 kernel trace
+       Q="--configs C4,C3s8 --no-cpu-baseline --no-conv --ar-probe 0 --steps 10 --warmup 1"
+       $J "test:tests/test_gpu_parity.py tests/test_trajectories.py tests/test_hydro.py tests/test_engine_emu.py tests/test_bench_settings.py tests/test_distributed_gpu.py" && \
+       $J "bench:r06_s39_a:$Q" && $J "bench:r06_s39_b:$Q" && $J "prof:r06_s39_c4_prof:--only C4 $A" ;;
   final) # the round's evidence: the whole GPU suite, smoke, the driver's default command, kernel traces
        $J "test:tests" && $J "py:r06_final_smoke:scripts/run_smoke.py" "bench:r06_final_default:--detail gpurun_out/r06_final_default_detail.json" \
           "prof:r06_final_prof:$H --ar-probe 0" "prof:r06_final_c3s8_prof:$S8" "prof:r06_final_1m_prof:$M" \
