@@ -526,6 +526,8 @@ def dominant_kernel(ph, K, fused):
                 # (the build that re-loads per round where the register build spills)
                 if small and "all=reload" in info:
                     kname = "phx_lane_all_rl"
+                elif small and "all=park" in info:
+                    kname = "phx_lane_all_pk"
             return (kname, st["lane_warm_ms"] / 1e3 / st["warm_launches"], st["warm_launches"],
                     lane_bytes(b, fused=bool(st.get("fused")) and fused), b.S)
         if "workgroup solver on" in info:

@@ -357,6 +357,17 @@ inline std::string lane_kernel_source(const LaneStructure& L, int warm_waves = 1
          "  if (t < io.S) still = phx_lane::all_lane<PT, false>(io, t, rescue);\n"
          "  phx_lane::compact_lane(still, t, io.lanes_out, io.count_out);\n"
          "}\n";
+    // ... and its build with the warm and rescue rounds' data parked in LDS
+    // (as_rounds_pk; the host's default over _rl, PHX_ALL_BUILD=reload keeps _rl)
+    o << "extern \"C\" __global__ void __launch_bounds__(64, 1) phx_lane_all_pk(phx_lane::LaneIO io, int rescue) {\n"
+         "  __shared__ double pk[phx_lane::Data<PT>::PARK * 64];\n"
+         "  if (phx_lane::gated(io.gate)) return;\n"
+         "  phx_lane::zero_next_counts(io.counts_next);\n"
+         "  const int t = blockIdx.x * 64 + threadIdx.x;\n"
+         "  bool still = false;\n"
+         "  if (t < io.S) still = phx_lane::all_lane<PT, false, true>(io, t, rescue, pk);\n"
+         "  phx_lane::compact_lane(still, t, io.lanes_out, io.count_out);\n"
+         "}\n";
     // phx_iterk fused mode, after the last enqueued iteration: the decision on
     // its conv (the next warm launch's prologue does it otherwise)
     // (and the copies the host reads after the drain, whether or not the loop

@@ -1698,6 +1698,29 @@ PHX_LD bool as_rounds(const LaneIO& io, int sc, ASet<PT>& a, int rounds, double*
     }
     return false;
 }
+// ... with the round data parked in LDS (pk: Data::PARK x 64 doubles, this
+// lane's column threadIdx.x; one wavefront per block) at the first round and
+// re-read from there per later round instead of re-loaded from memory: a
+// lone lane's rounds (the rescue tails) paid the loads' and the x-bar
+// gather's round trips every round.  The same values, so the same results.
+#if defined(__HIPCC__) || defined(__HIPCC_RTC__)
+template <class PT>
+PHX_LD bool as_rounds_pk(const LaneIO& io, int sc, ASet<PT>& a, int rounds, double* xp, double* z, double* pk) {
+    const int lane = (int)threadIdx.x;
+    if (rounds > 0) {
+        const Data<PT> D0(io, sc);
+        D0.park(pk, lane);
+    }
+    PHX_NOUNROLL for (int r = 0; r < rounds; ++r) {
+        const Data<PT> D(io, sc, pk, lane);
+        const int c = as_round<PT>(io, D, a, xp, z, r);
+        if (c == 3) return false;
+        if (c == 0) return true;
+        if (c == 2) { PHX_LANE_STAT(3); return false; }
+    }
+    return false;
+}
+#endif
 
 // ---------------------------------------------------------------------------
 // Iter0 seeding (phx_kernels.hip enqueue_seeded_solve): T template lanes spread
@@ -1813,13 +1836,22 @@ PHX_LD void write_certified(const LaneIO& io, const Data<PT>& D, int sc, const A
     aset_store<PT>(io, sc, a);
 }
 
+// the warm pass's rounds: re-loaded per round, or parked (PK, GPU only)
+template <class PT, bool PK>
+PHX_LD bool warm_rounds_of(const LaneIO& io, int sc, ASet<PT>& a, double* xp, double* z, double* pk) {
+#if defined(__HIPCC__) || defined(__HIPCC_RTC__)
+    if constexpr (PK) return as_rounds_pk<PT>(io, sc, a, io.warm_rounds, xp, z, pk);
+#endif
+    return as_rounds<PT>(io, sc, a, io.warm_rounds, xp, z);
+}
+
 // ---------------------------------------------------------------------------
 // Kernel bodies.  Both return true if the lane still needs the generic path.
 // ---------------------------------------------------------------------------
 // REG: every round on the data loaded at entry (one wave per SIMD kernels with
 // the whole register file, phx_lane_warm_list: no per-round re-load)
-template <class PT, bool MAP = true, bool REG = false>
-PHX_LD bool warm_lane(const LaneIO& io, int sc) {
+template <class PT, bool MAP = true, bool REG = false, bool PK = false>
+PHX_LD bool warm_lane(const LaneIO& io, int sc, double* pk = nullptr) {
     constexpr int NN = PT::NMAX_N, MM = PT::NMAX_M;
     const Data<PT> D(io, sc);
     ASet<PT> a;
@@ -1847,7 +1879,7 @@ PHX_LD bool warm_lane(const LaneIO& io, int sc) {
             }
             if (c != 1) { PHX_LANE_STAT(3); break; }
         }
-    } else if (as_rounds<PT>(io, sc, a, io.warm_rounds, xp, z)) {
+    } else if (warm_rounds_of<PT, PK>(io, sc, a, xp, z, pk)) {
         const Data<PT> Dc(io, opaque_index(sc));
         const bool mok = MAP && io.map && map_compute<PT>(Dc, a, io, sc);
         write_certified<PT>(io, Dc, sc, a, xp, z, 0, mok);
@@ -1995,14 +2027,16 @@ PHX_LD bool cold_rounds_lane(const LaneIO& io, int sc) {
 #else
 #define PHX_ALL_REG_DEF true
 #endif
-template <class PT, bool REG = PHX_ALL_REG_DEF>
-PHX_LD bool all_lane(const LaneIO& io, int sc, int rescue) {
-    if (!warm_lane<PT, false, REG>(io, sc)) return false;
+// PK (with REG false; phx_lane_all_pk): the warm and rescue rounds on data
+// parked in LDS (as_rounds_pk; pk: Data::PARK x 64 doubles of the block's LDS)
+template <class PT, bool REG = PHX_ALL_REG_DEF, bool PK = false>
+PHX_LD bool all_lane(const LaneIO& io, int sc, int rescue, double* pk = nullptr) {
+    if (!warm_lane<PT, false, REG, PK>(io, sc, pk)) return false;
     if (rescue > 0) {
         LaneIO io2 = io;
         io2.warm_rounds = rescue;
         io2.single_after = 1;
-        if (!warm_lane<PT, false, REG>(io2, sc)) return false;
+        if (!warm_lane<PT, false, REG, PK>(io2, sc, pk)) return false;
     }
     LaneIO io3 = io;
     io3.single_after = 1;          // (the cold pass after warm passes: single changes, phx_kernels.hip)

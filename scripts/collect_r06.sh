@@ -12,7 +12,7 @@ $S phx_lane_warm_fzr2 --last 49 $G/r06_pmc_c3_sq > $P/r06_pmcsq_farmer100k_phx_l
 $S phx_lane_warm_fz1 --last 19 $G/r06_pmc_s8_fetch $G/r06_pmc_s8_write > $P/r06_pmc_farmer12k5_phx_lane_warm_fz1.json
 $S phx_lane_warm_fz1 --last 19 $G/r06_pmc_s8_sq > $P/r06_pmcsq_farmer12k5_phx_lane_warm_fz1.json
 $S phx_lane_warm_fzr2 --last 19 $G/r06_pmc_1m_fetch $G/r06_pmc_1m_write > $P/r06_pmc_farmer1m_phx_lane_warm_fzr2.json
-$S phx_lane_all_rl --last 10 $G/r06_pmc_c4_fetch $G/r06_pmc_c4_write > $P/r06_pmc_aircond1k_phx_lane_all_rl.json
+$S phx_lane_all_pk --last 10 $G/r06_pmc_c4_fetch $G/r06_pmc_c4_write > $P/r06_pmc_aircond1k_phx_lane_all_pk.json
 $S k_wg_warm --last 10 --skip-idle $G/r06_pmc_c2_fetch $G/r06_pmc_c2_write > $P/r06_pmc_farmercm10_1k_k_wg_warm.json
 $S k_wg_warm --last 10 --skip-idle $G/r06_pmc_c5a_fetch $G/r06_pmc_c5a_write > $P/r06_pmc_sslp10k_k_wg_warm.json
 $S k_sp_solve --last 10 --skip-idle $G/r06_pmc_c5b_fetch $G/r06_pmc_c5b_write > $P/r06_pmc_netdes10k_k_sp_solve.json

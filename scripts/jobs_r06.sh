@@ -171,6 +171,34 @@ case "$1" in
        Q="--configs C4,C3s8 --no-cpu-baseline --no-conv --ar-probe 0 --steps 10 --warmup 1"
        $J "test:tests/test_gpu_parity.py tests/test_trajectories.py tests/test_hydro.py tests/test_engine_emu.py tests/test_bench_settings.py tests/test_distributed_gpu.py" && \
        $J "bench:r06_s39_a:$Q" && $J "bench:r06_s39_b:$Q" && $J "prof:r06_s39_c4_prof:--only C4 $A" ;;
+  s40) # k_small_xw's run scans as DPP steps (no ds_bpermute), prev_left loaded at entry: parity, C4 twice, C4 trace
+       Q="--configs C4,C3s8 --no-cpu-baseline --no-conv --ar-probe 0 --steps 10 --warmup 1"
+       $J "test:tests/test_gpu_parity.py tests/test_trajectories.py tests/test_hydro.py tests/test_engine_emu.py tests/test_bench_settings.py tests/test_distributed_gpu.py" && \
+       $J "bench:r06_s40_a:$Q" && $J "bench:r06_s40_b:$Q" && $J "prof:r06_s40_c4_prof:--only C4 $A" ;;
+  s41) # + k_small_xw's node fold with one LDS round trip per entry, Iter0's copies and sums in one launch for
+       # S <= 8192 (k_iter0_keep1): parity, C4 twice, C4 trace
+       Q="--configs C4,C3s8 --no-cpu-baseline --no-conv --ar-probe 0 --steps 10 --warmup 1"
+       $J "test:tests" && \
+       $J "bench:r06_s41_a:$Q" && $J "bench:r06_s41_b:$Q" && $J "prof:r06_s41_c4_prof:--only C4 $A" ;;
+  s42) # k_small_xw: the node fold four wavefronts per LDS round trip (s41's sixteen raised it to 17.3 us), the
+       # convergence sum unrolled in registers (no scratch); C4 twice, C4 trace
+       Q="--configs C4,C3s8 --no-cpu-baseline --no-conv --ar-probe 0 --steps 10 --warmup 1"
+       $J "bench:r06_s42_a:$Q" && $J "bench:r06_s42_b:$Q" && $J "prof:r06_s42_c4_prof:--only C4 $A" ;;
+  s43) # phx_lane_all_pk (the warm and rescue rounds' data parked in LDS) against phx_lane_all_rl: the aircond
+       # parity tests with the park build forced, C4 alternating, C4 trace of the park build
+       Q="--configs C4 --no-cpu-baseline --no-conv --ar-probe 0 --steps 10 --warmup 1"
+       P="PHX_ALL_BUILD=park"
+       env $P $J "test:tests -k aircond" && \
+       env $P $J "bench:r06_s43_p:$Q" && $J "bench:r06_s43_r:$Q" && env $P $J "bench:r06_s43_p2:$Q" && \
+       $J "bench:r06_s43_r2:$Q" && env $P $J "prof:r06_s43_c4_prof:--only C4 $A" ;;
+  s44) # phx_lane_all_pk the default where phx_lane_all spills; the unfused loop's tail copies as one kernel
+       # (k_tail_copy): the whole GPU suite, C4 / C3s8 twice, C4 trace
+       Q="--configs C4,C3s8 --no-cpu-baseline --no-conv --ar-probe 0 --steps 10 --warmup 1"
+       $J "test:tests" && $J "bench:r06_s44_a:$Q" && $J "bench:r06_s44_b:$Q" && $J "prof:r06_s44_c4_prof:--only C4 $A" ;;
+  s45) # s44 rebuilt (s44's library predates the park default): the aircond and iterk tests, C4 / C3s8 twice, C4 trace
+       Q="--configs C4,C3s8 --no-cpu-baseline --no-conv --ar-probe 0 --steps 10 --warmup 1"
+       $J "test:tests -k aircond" && $J "bench:r06_s45_a:$Q" && $J "bench:r06_s45_b:$Q" && \
+       $J "prof:r06_s45_c4_prof:--only C4 $A" ;;
   final) # the round's evidence: the whole GPU suite, smoke, the driver's default command, kernel traces
        $J "test:tests" && $J "py:r06_final_smoke:scripts/run_smoke.py" "bench:r06_final_default:--detail gpurun_out/r06_final_default_detail.json" \
           "prof:r06_final_prof:$H --ar-probe 0" "prof:r06_final_c3s8_prof:$S8" "prof:r06_final_1m_prof:$M" \

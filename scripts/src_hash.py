@@ -13,6 +13,7 @@ _LANE = ["phx_lane.h", "phx_jit.h", "phx_setup.h", "phx_kernels.hip"]
 KERNEL_SOURCES = {
     "phx_lane_warm": _LANE, "phx_lane_warm_fz": _LANE, "phx_lane_warm_fz1": _LANE, "phx_lane_all": _LANE,
     "phx_lane_all_rl": _LANE,
+    "phx_lane_all_pk": _LANE,
     "phx_lane_warm_fzr2": _LANE, "phx_lane_warm_fzc": _LANE,
     "k_wg_warm": ["phx_wg.h", "phx_core.h", "phx_setup.h", "phx_kernels.hip"],
     "k_sp_solve": ["phx_sp.h", "phx_core.h", "phx_setup.h", "phx_kernels.hip"],

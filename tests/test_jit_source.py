@@ -22,7 +22,7 @@ _CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 _HIPRTC = "/opt/rocm/lib/libhiprtc.so"
 KERNELS = ["phx_lane_cold", "phx_lane_cold_as", "phx_lane_warm", "phx_lane_warm_list", "phx_lane_map",
            "phx_fz_tail", "phx_lane_seed", "phx_lane_warm_fz", "phx_lane_warm_fz1", "phx_lane_all",
-           "phx_lane_list_all", "phx_lane_all_rl"]
+           "phx_lane_list_all", "phx_lane_all_rl", "phx_lane_all_pk"]
 
 
 def hiprtc_compile(src):
