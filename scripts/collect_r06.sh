@@ -20,7 +20,7 @@ for t in prof c3s8_prof 1m_prof c2_prof c4_prof c5a_prof c5b_prof; do
   cp $G/r06_final_$t/run_kernel_stats.csv $P/r06_final_${t%_prof}_kernel_stats.csv
 done
 mv $P/r06_final_prof_kernel_stats.csv $P/r06_final_headline_kernel_stats.csv 2>/dev/null || true
-cp $G/r06_final2_default.log $P/r06_final_bench_default.log
-cp $G/r06_final2_default_detail.json $P/r06_final_bench_default_detail.json
+cp $G/r06_final_default.log $P/r06_final_bench_default.log
+cp $G/r06_final_default_detail.json $P/r06_final_bench_default_detail.json
 cp $G/test_1.log $P/r06_final_pytest_gpu_all.log 2>/dev/null || true
 cp $G/r06_final_smoke.log $P/r06_final_smoke.log 2>/dev/null || true
