@@ -111,6 +111,32 @@ def test_aircond_bf10x10x10_multi_change_gpu(gpu_lib):
     assert len(runs[MULTI_SETTING[0]][0].xbar_by_node()) == 111
 
 
+@pytest.mark.gpu
+def test_aircond_all_builds_bit_equal_gpu(gpu_lib, monkeypatch):
+    """The small-batch whole-solve kernel's three builds (phx_lane_all: the
+    register build; _rl: its data re-loaded per round; _pk: parked in LDS, the
+    default where the register build spills) run the same per-lane arithmetic
+    on the same values: x, W, x-bar and conv bit for bit equal on configs[3]
+    with the bench's C4 setting, and each build is the one that ran."""
+    bfs = [10, 10, 10]
+    names = ["scen%d" % i for i in range(int(np.prod(bfs)))]
+    nodes = sputils.create_nodenames_from_branching_factors(bfs)
+    so = {"lane_multi_theta": MULTI_SETTING[0], "lane_multi_rounds": MULTI_SETTING[1]}
+    out = {}
+    for build, tag in (("reg", ""), ("reload", "all=reload"), ("park", "all=park")):
+        monkeypatch.setenv("PHX_ALL_BUILD", build)
+        ph, conv, Eobj, tb = run_engine(aircond.scenario_creator, names, {"branching_factors": bfs}, 4,
+                                        lib=gpu_lib, all_nodenames=nodes,
+                                        options={"iter0_solver_options": so, "iterk_solver_options": so})
+        info = ph._native.jit_info(ph._ctx).decode()
+        assert (tag in info) if tag else ("all=" not in info), info
+        assert all_certified(ph)
+        out[build] = (ph._host("x"), ph.W_array(), conv, Eobj)
+    for build in ("reload", "park"):
+        for a, b in zip(out["reg"], out[build]):
+            assert np.array_equal(np.asarray(a), np.asarray(b)), build
+
+
 def test_docs_farmer_via_engine(emu):
     """doc/src/examples.rst trajectory (rho 10, 5 iterations) through the engine."""
     from mpisppy_amd import model as lm
