@@ -199,6 +199,9 @@ case "$1" in
        Q="--configs C4,C3s8 --no-cpu-baseline --no-conv --ar-probe 0 --steps 10 --warmup 1"
        $J "test:tests -k aircond" && $J "bench:r06_s45_a:$Q" && $J "bench:r06_s45_b:$Q" && \
        $J "prof:r06_s45_c4_prof:--only C4 $A" ;;
+  s47) # C4 on the final sources, three runs on one box (the box-to-box spread of the step)
+       Q="--configs C4 --no-cpu-baseline --no-conv --ar-probe 0 --steps 10 --warmup 1"
+       $J "bench:r06_s47_a:$Q" && $J "bench:r06_s47_b:$Q" && $J "bench:r06_s47_c:$Q" ;;
   final) # the round's evidence: the whole GPU suite, smoke, the driver's default command, kernel traces
        $J "test:tests" && $J "py:r06_final_smoke:scripts/run_smoke.py" "bench:r06_final_default:--detail gpurun_out/r06_final_default_detail.json" \
           "prof:r06_final_prof:$H --ar-probe 0" "prof:r06_final_c3s8_prof:$S8" "prof:r06_final_1m_prof:$M" \
