@@ -202,6 +202,9 @@ case "$1" in
   s47) # C4 on the final sources, three runs on one box (the box-to-box spread of the step)
        Q="--configs C4 --no-cpu-baseline --no-conv --ar-probe 0 --steps 10 --warmup 1"
        $J "bench:r06_s47_a:$Q" && $J "bench:r06_s47_b:$Q" && $J "bench:r06_s47_c:$Q" ;;
+  s48) # C4 inside the default run against C4 alone, one box (is the default run's C4 slower by its order?)
+       Q="--configs C4 --no-cpu-baseline --no-conv --ar-probe 0 --steps 10 --warmup 1"
+       $J "bench:r06_s48_def:" && $J "bench:r06_s48_c4:$Q" && $J "bench:r06_s48_c4b:$Q" ;;
   final) # the round's evidence: the whole GPU suite, smoke, the driver's default command, kernel traces
        $J "test:tests" && $J "py:r06_final_smoke:scripts/run_smoke.py" "bench:r06_final_default:--detail gpurun_out/r06_final_default_detail.json" \
           "prof:r06_final_prof:$H --ar-probe 0" "prof:r06_final_c3s8_prof:$S8" "prof:r06_final_1m_prof:$M" \
